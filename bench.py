@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of the path-tracing hot path (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): input box.gltf (Cornell box), 1920x1080,
+1024 spp, 8 bounces, seed 42, one frame per step == PathTracer::doTrace
+(path_tracer.cu:491-554): setupRandSeed + all spp of the trace megakernel +
+copyToFB, inputs resident in HBM.  A "ray" is one traverseBVH call (primary,
+extension, direct probe, shadow), counted by the kernel.
+
+N GPUs: one process per GPU (torch.distributed.run), the frame is split in
+interleaved 16-row bands, each rank renders its band, one gather (RCCL) brings
+the bands to rank 0 inside the timed region.  Strong scaling (the frame is
+fixed).  value = rays of the whole frame / max-over-ranks step time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+# algorithmic bytes: internal visit = links 8 + 2 child AABBs 48;
+# leaf = fid 4 + 3 indices 12 + 3 vertices 36; shading hit = 3 normals 36 +
+# 3 indices 12 + material 60; pixel write = 12
+B_INNER, B_LEAF, B_HIT, B_PIX = 56, 52, 108, 12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="box")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--band-rows", type=int, default=16)
+    ap.add_argument("--spp-per-launch", type=int, default=0)
+    ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port on rank 0 at N=1")
+    ap.add_argument("--cpu-spp", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_trace_latest.json"),
+                    help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/profile.sh)")
+    return ap.parse_args()
+
+
+def scene_file(name):
+    p = os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.gltf")
+    if not os.path.exists(p):
+        p = name
+    return p
+
+
+def cpu_baseline(args):
+    """The oracle (CPU port of the reference kernels) on the host cores, same
+    scene/resolution/depth, bounded spp; trace phase only (RNG init reported
+    separately, like the reference's per-frame curand_init)."""
+    from oracle import oracle as O
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    ps = O.load_scene(scene_file(args.scene))
+    _, _, c = O.render(ps, args.width, args.height, args.cpu_spp, args.depth, args.seed, trig_mode=1,
+                       threads=threads)
+    mrays = c["traversals"] / (c["trace_ms"] * 1e3)
+    return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{args.scene}.gltf {args.width}x{args.height} x {args.cpu_spp} spp, depth {args.depth}, "
+                      f"seed {args.seed}: {c['traversals']} rays in {c['trace_ms'] / 1e3:.2f} s trace "
+                      f"(+{c['init_ms'] / 1e3:.2f} s RNG init not counted)",
+            "cpu_model": _cpu_model()}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import tinypathtracer_amd as T
+    from tinypathtracer_amd import shard
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = local
+    torch.cuda.set_device(dev)
+
+    scene = T.Scene(scene_file(args.scene))
+    d_scene = scene.copySceneToDevice(dev)
+    t0 = time.perf_counter()
+    d_scene.build()
+    build_ms = (time.perf_counter() - t0) * 1e3
+    W, H = args.width, args.height
+    pt = T.PathTracer("", W, H, dev)
+    radiance = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
+    band = (args.band_rows, world, rank)
+
+    def step():
+        st = pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,
+                        radiance=radiance, band=band, spp_per_launch=args.spp_per_launch,
+                        flags=args.flags)
+        frame = shard.gather_frame(radiance, H, args.band_rows, world, rank) if world > 1 else radiance
+        return st, frame
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    stats = []
+    for _ in range(args.steps):
+        st, frame = step()
+        stats.append(st)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    keys = ["traversals", "internal_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
+            "rng_init_ms", "resolve_ms", "trace_launches"]
+    local_tot = {k: float(sum(s[k] for s in stats)) for k in keys}
+    vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+    if world > 1:
+        mx = vec.clone()
+        dist.all_reduce(vec, op=dist.ReduceOp.SUM)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        elapsed = float(mx[-1].item())
+        tot = {k: float(vec[i].item()) for i, k in enumerate(keys)}
+        tot["trace_ms_max"] = float(mx[keys.index("trace_ms")].item())
+        tot["trace_launches_max"] = float(mx[keys.index("trace_launches")].item())
+    else:
+        tot = dict(local_tot)
+        tot["trace_ms_max"] = tot["trace_ms"]
+        tot["trace_launches_max"] = tot["trace_launches"]
+
+    if rank == 0:
+        K = args.steps
+        rays = tot["traversals"]
+        value = rays / elapsed / 1e6
+        # roofline of the dominant kernel (k_trace), per launch, rank 0's device
+        l_tot = local_tot
+        nl = max(l_tot["trace_launches"], 1.0)
+        bytes_total = (B_INNER * l_tot["internal_visits"] + B_LEAF * l_tot["leaf_tests"] +
+                       B_HIT * l_tot["shade_hits"] + B_PIX * l_tot["pixels"])
+        bytes_per_launch = bytes_total / nl
+        avg_launch_s = (l_tot["trace_ms"] / nl) / 1e3
+        achieved = bytes_per_launch / avg_launch_s / 1e9
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            try:
+                with open(args.pmc_json) as f:
+                    pm = json.load(f)
+                traffic = pm.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        out = {
+            "metric": "Mrays/s at 1920x1080x1024spp (box.gltf, 8 bounces); achieved algorithmic GB/s vs HBM peak",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "reference asset input/box.gltf (tests/golden/scenes), seed 42, no env map (black miss)",
+            "config": {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}",
+                       "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
+                       "max_depth": args.depth, "seed": args.seed,
+                       "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + RCCL gather"
+                       if world > 1 else "1 GPU"},
+            "msamples_per_s": round(tot["samples"] / elapsed / 1e6, 2),
+            "rays_per_sample": round(rays / max(tot["samples"], 1), 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "k_trace", "bytes_per_launch": bytes_per_launch,
+                         "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "launches_per_step": nl / K},
+            "phases_ms_per_step": {"rng_init": round(l_tot["rng_init_ms"] / K, 3),
+                                   "trace": round(l_tot["trace_ms"] / K, 3),
+                                   "resolve": round(l_tot["resolve_ms"] / K, 3),
+                                   "bvh_build_once": round(build_ms, 3)},
+        }
+        if world == 1 and args.cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

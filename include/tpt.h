@@ -1,0 +1,170 @@
+/*
+ * tpt.h -- C-ABI of the MI355X-native TinyPathTracer hot path (libtpt.so).
+ *
+ * Drop-in boundary for the reference's render job
+ *   PathTracer::doTrace(DeviceScene&, Camera&, unsigned char* fb, int spp)
+ *   (include/path_tracer.h:34, src/path_tracer.cu:491-554)
+ * and for the device ABI of its `trace` kernel
+ *   (src/path_tracer.cu:296-299).  Plain pointers and sizes only; no
+ * exceptions cross this boundary (errors: tpt_status + tpt_last_error()).
+ *
+ * Handles own device memory; caller buffers are borrowed.  One tpt_scene per
+ * HIP device; calls on different scenes may run concurrently from different
+ * host threads, calls on one scene must be serialised by the caller.
+ */
+#ifndef TPT_H
+#define TPT_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPT_VERSION_MAJOR 0
+#define TPT_VERSION_MINOR 1
+
+typedef enum {
+    TPT_OK = 0,
+    TPT_ERR_INVALID_ARG = 1,
+    TPT_ERR_HIP = 2,
+    TPT_ERR_OOM = 3,
+    TPT_ERR_IO = 4,
+    TPT_ERR_PARSE = 5,
+    TPT_ERR_NO_DEVICE = 6
+} tpt_status;
+
+/* Material, 60 bytes: the reference's Material (include/material.h:86-120). */
+typedef struct {
+    float base_color[3];
+    float emission_factor;
+    float eta;
+    float metallic;
+    float subsurface, specular, roughness, specular_tint, anisotropic,
+          sheen, sheen_tint, clearcoat, clearcoat_gloss;
+} tpt_material;
+
+/* DeltaLight flattened (include/delta_light.h:35-130); type 0 point,
+ * 1 directional, 2 spot.  Intensities already in the reference's units
+ * (point/spot lumens x 1/683, mesh.cu:276,290). */
+typedef struct {
+    int32_t type;
+    float color[3];
+    float intensity;
+    float pos[3];
+    float direction[3];
+    float cos_outer;
+    float inv_cos_cone_diff;
+} tpt_light;
+
+/* MtlInterval (include/mesh.cuh:74-78): object o owns faces [begin, next begin). */
+typedef struct {
+    int32_t begin;
+    int32_t mtl;
+} tpt_interval;
+
+/* Host-side scene, the content of DeviceScene (include/mesh.cuh:80-96). */
+typedef struct {
+    const uint32_t* indices;      uint32_t n_faces;      /* 3*n_faces global vertex ids */
+    const float* vertices;        const float* normals;  uint32_t n_vertices; /* xyz, object space */
+    const tpt_interval* lut;      uint32_t n_objects;
+    const float* vert_trans;      const float* normal_trans; /* 16 floats/object, column-major */
+    const tpt_material* materials; uint32_t n_materials;   /* empty -> Material() default */
+    const tpt_light* lights;      uint32_t n_lights;
+} tpt_scene_desc;
+
+/* Camera (include/camera.h): c2w = m_transform->localToWorld(). */
+typedef struct {
+    float c2w[16];      /* column-major */
+    float vfov;         /* radians */
+    float aspect;       /* camera aspect ratio (the reference ignores W/H here) */
+    float znear;
+} tpt_camera;
+
+typedef struct {
+    int32_t width, height;        /* full frame */
+    int32_t spp;                  /* samples per pixel (reference: 64 per frame) */
+    int32_t max_depth;            /* DEPTH_TRACE (reference: 8), 1..64 */
+    uint64_t seed;                /* curand_init seed (reference: time()) */
+    /* Interleaved row bands for multi-GPU sharding: this call renders rows y
+     * with (y / band_rows) % band_count == band_index.  band_count 1 = all. */
+    int32_t band_rows, band_count, band_index;
+    int32_t spp_per_launch;       /* 0 = auto; chunks the spp loop over launches */
+    int32_t flags;                /* TPT_FLAG_* */
+} tpt_params;
+
+#define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
+#define TPT_FLAG_REF_ORDER     0x2   /* reference right-first traversal, no culling */
+
+typedef struct {
+    uint64_t traversals;          /* traverseBVH calls: primary+extension+probe+shadow */
+    uint64_t internal_visits;     /* internal nodes popped */
+    uint64_t leaf_tests;          /* leaves popped (triangle tests) */
+    uint64_t shade_hits;          /* extension-ray hits shaded */
+    uint64_t pixels;              /* pixels rendered by this call */
+    uint64_t samples;             /* pixels * spp */
+    double rng_init_ms;           /* setupRandSeed equivalent */
+    double trace_ms;              /* sum over trace launches (HIP events) */
+    double resolve_ms;            /* copyToFB equivalent */
+    double total_ms;              /* whole tpt_render, host wall */
+    int32_t trace_launches;
+    int32_t pad;
+} tpt_stats;
+
+typedef struct tpt_scene tpt_scene;
+typedef struct tpt_env tpt_env;
+
+/* Library identity and errors. */
+const char* tpt_version(void);
+const char* tpt_last_error(void);
+int tpt_device_count(void);
+
+/* Upload a scene to `device` (hipSetDevice index).  Replaces
+ * Scene::copySceneToDevice (mesh.cu:309-397). */
+tpt_status tpt_scene_create(const tpt_scene_desc* desc, int device, tpt_scene** out);
+/* World transform + LBVH build on the device (path_tracer.cu:536-542,
+ * bvh.cu:304-331) and the packed traversal layout. */
+tpt_status tpt_scene_build(tpt_scene* scene);
+void tpt_scene_destroy(tpt_scene* scene);
+
+/* Equirect environment, RGBA8, row 0 = bottom (FreeImage order), already in
+ * RGB channel order (texture.cu:33-47 swizzle applied by the caller). */
+tpt_status tpt_env_create(const uint8_t* rgba, int32_t width, int32_t height, int device, tpt_env** out);
+void tpt_env_destroy(tpt_env* env);
+
+/* One frame == doTrace: setupRandSeed, trace (spp), copyToFB.
+ *   radiance_out: nullable, width*height*3 floats = color/spp, row 0 = bottom;
+ *                 host or device pointer (detected).  Only band rows written.
+ *   bgra_out:     nullable, width*height*4 bytes, row 0 = top, B,G,R written,
+ *                 alpha untouched (copyToFB, path_tracer.cu:451-471).
+ *   env:          nullable -> black on miss. */
+tpt_status tpt_render(tpt_scene* scene, const tpt_env* env, const tpt_camera* camera,
+                      const tpt_params* params, float* radiance_out, uint8_t* bgra_out,
+                      tpt_stats* stats);
+
+/* Introspection for tests: copy back the built BVH in the reference node
+ * layout (bvh.cuh:52-58, 36 B/node, 2F-1 nodes) and the sorted Morton keys. */
+tpt_status tpt_scene_read_bvh(tpt_scene* scene, void* nodes36, int64_t* keys);
+/* World-space vertices / normals after tpt_scene_build (n_vertices*3 each). */
+tpt_status tpt_scene_read_world(tpt_scene* scene, float* wverts, float* wnorms);
+/* Per-pixel RNG states after setupRandSeed for the first n pixels: 6 words
+ * each {v0..v4, d}. */
+tpt_status tpt_debug_rng_init(int device, uint64_t seed, uint64_t first_pixel, uint32_t n, uint32_t* states);
+/* Trace n rays (origins/dirs xyz) against the built BVH: hit fid (-1 miss), t, u, v. */
+tpt_status tpt_debug_trace_rays(tpt_scene* scene, uint32_t n, const float* origins, const float* dirs,
+                                int32_t* hit, float* t, float* uv);
+
+/* ---- host-side glTF loader (mesh.cu:80-397 semantics) -------------------- */
+typedef struct tpt_gltf tpt_gltf;
+tpt_status tpt_gltf_load(const char* path, tpt_gltf** out);
+/* Borrowed views valid until tpt_gltf_free. */
+tpt_status tpt_gltf_desc(const tpt_gltf* g, tpt_scene_desc* desc, tpt_camera* camera);
+/* 1 if a mesh had no material (reference reads out of bounds; we use Material()). */
+int tpt_gltf_missing_material(const tpt_gltf* g);
+void tpt_gltf_free(tpt_gltf* g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPT_H */

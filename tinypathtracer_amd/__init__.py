@@ -1,0 +1,329 @@
+"""tinypathtracer_amd -- MI355X-native TinyPathTracer hot path, Python host mirror.
+
+Mirrors the reference host API (include/path_tracer.h:16-35,
+include/mesh.cuh:98-115, include/bvh.cuh:60-68, include/camera.h) over the
+C-ABI in include/tpt.h (libtpt.so, HIP for gfx950):
+
+    pt = PathTracer(env_file)            # PathTracer(const std::string&)
+    frame = pt.render("input/box.gltf")  # render(meshFile), headless
+
+Scene/Mesh loading, BVH construction and the trace megakernel all run in the
+native library; this module only marshals arrays.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import TPTError, check, lib
+
+__all__ = ["Camera", "Scene", "DeviceScene", "BVH", "EnvLight", "PathTracer", "Frame", "TPTError",
+           "procedural_sky", "version", "device_count", "NODE_DTYPE"]
+
+# BVHNode (include/bvh.cuh:52-58): parent, info{left,right | fid,placeHolder}, box
+NODE_DTYPE = np.dtype([("parent", "<u4"), ("a", "<i4"), ("b", "<i4"), ("bmin", "<f4", 3), ("bmax", "<f4", 3)])
+
+
+def version() -> str:
+    return lib().tpt_version().decode()
+
+
+def device_count() -> int:
+    return int(lib().tpt_device_count())
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+@dataclass
+class Camera:
+    """include/camera.h:9-65 (getters :56-58); c2w = m_transform->localToWorld()."""
+    c2w: np.ndarray
+    vfov: float
+    aspect: float
+    znear: float = 0.1
+
+    def getVFov(self):
+        return self.vfov
+
+    def getAspRatio(self):
+        return self.aspect
+
+    def getNearPlane(self):
+        return self.znear
+
+    def to_c(self) -> _lib.Camera:
+        c = _lib.Camera()
+        c.c2w[:] = [float(v) for v in np.asarray(self.c2w, np.float32).reshape(16)]
+        c.vfov, c.aspect, c.znear = float(self.vfov), float(self.aspect), float(self.znear)
+        return c
+
+
+class Scene:
+    """Scene(filename, type) (mesh.cu:68-79): host-side glTF scene, loaded by the
+    native loader (mesh.cu:80-307 semantics).  Arrays are the packed content of
+    copySceneToDevice (mesh.cu:309-397)."""
+
+    def __init__(self, filename: str, type: str = "gltf"):
+        if type != "gltf":
+            raise RuntimeError("Unsupported file format. Only support .gltf file.")
+        h = C.c_void_p()
+        check(lib().tpt_gltf_load(os.fsencode(filename), C.byref(h)))
+        try:
+            d = _lib.SceneDesc()
+            cam = _lib.Camera()
+            check(lib().tpt_gltf_desc(h, C.byref(d), C.byref(cam)))
+            nf, nv = d.n_faces, d.n_vertices
+            self.indices = np.ctypeslib.as_array(d.indices, (3 * nf,)).copy()
+            self.vertices = np.ctypeslib.as_array(d.vertices, (nv, 3)).copy()
+            self.normals = np.ctypeslib.as_array(d.normals, (nv, 3)).copy()
+            self.lut = np.array([(d.lut[i].begin, d.lut[i].mtl) for i in range(d.n_objects)], np.int32)
+            self.vert_trans = np.ctypeslib.as_array(d.vert_trans, (d.n_objects, 16)).copy()
+            self.normal_trans = np.ctypeslib.as_array(d.normal_trans, (d.n_objects, 16)).copy()
+            self.materials = np.array([[*d.materials[i].base_color] + [getattr(d.materials[i], f)
+                                        for f, _ in _lib.Material._fields_[1:]] for i in range(d.n_materials)],
+                                      np.float32).reshape(-1, 15)
+            self.lights = [_lib.Light.from_buffer_copy(d.lights[i]) for i in range(d.n_lights)]
+            self.missing_material = bool(lib().tpt_gltf_missing_material(h))
+            self.m_camera = Camera(np.array(cam.c2w[:], np.float32), cam.vfov, cam.aspect, cam.znear)
+        finally:
+            lib().tpt_gltf_free(h)
+        self.filename = filename
+
+    @property
+    def n_faces(self):
+        return len(self.indices) // 3
+
+    def desc(self):
+        """tpt_scene_desc view (keeps buffers alive on self)."""
+        self._mats = (_lib.Material * max(len(self.materials), 1))()
+        for i, row in enumerate(self.materials):
+            m = self._mats[i]
+            m.base_color[:] = [float(v) for v in row[:3]]
+            for k, (f, _) in enumerate(_lib.Material._fields_[1:]):
+                setattr(m, f, float(row[3 + k]))
+        self._lights = (_lib.Light * max(len(self.lights), 1))(*self.lights)
+        self._lut = (_lib.Interval * len(self.lut))(*[_lib.Interval(int(b), int(m)) for b, m in self.lut])
+        self._arr = [np.ascontiguousarray(a) for a in (self.indices, self.vertices, self.normals,
+                                                        self.vert_trans, self.normal_trans)]
+        ind, ver, nor, vt, nt = self._arr
+        return _lib.SceneDesc(
+            ind.ctypes.data_as(C.POINTER(C.c_uint32)), self.n_faces,
+            ver.ctypes.data_as(C.POINTER(C.c_float)), nor.ctypes.data_as(C.POINTER(C.c_float)), len(ver),
+            C.cast(self._lut, C.POINTER(_lib.Interval)), len(self.lut),
+            vt.ctypes.data_as(C.POINTER(C.c_float)), nt.ctypes.data_as(C.POINTER(C.c_float)),
+            C.cast(self._mats, C.POINTER(_lib.Material)), len(self.materials),
+            C.cast(self._lights, C.POINTER(_lib.Light)), len(self.lights))
+
+    def copySceneToDevice(self, device: int = 0) -> "DeviceScene":
+        return DeviceScene(self, device)
+
+
+class DeviceScene:
+    """DeviceScene (mesh.cuh:80-96): scene buffers resident in HBM of `device`."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        self.scene = scene
+        self.device = device
+        self.handle = C.c_void_p()
+        d = scene.desc()
+        check(lib().tpt_scene_create(C.byref(d), device, C.byref(self.handle)))
+        self.built = False
+
+    def build(self):
+        """World transform + LBVH (path_tracer.cu:536-542) on the device."""
+        check(lib().tpt_scene_build(self.handle))
+        self.built = True
+        return self
+
+    def read_bvh(self):
+        nf = self.scene.n_faces
+        nodes = np.zeros(2 * nf - 1, NODE_DTYPE)
+        keys = np.zeros(nf, np.int64)
+        check(lib().tpt_scene_read_bvh(self.handle, _ptr(nodes), _ptr(keys)))
+        return nodes, keys
+
+    def read_world(self):
+        nv = len(self.scene.vertices)
+        wv = np.zeros((nv, 3), np.float32)
+        wn = np.zeros((nv, 3), np.float32)
+        check(lib().tpt_scene_read_world(self.handle, _ptr(wv), _ptr(wn)))
+        return wv, wn
+
+    def trace_rays(self, origins, dirs):
+        o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        n = len(o)
+        hit = np.zeros(n, np.int32)
+        t = np.zeros(n, np.float32)
+        uv = np.zeros((n, 2), np.float32)
+        check(lib().tpt_debug_trace_rays(self.handle, n, _ptr(o), _ptr(d), _ptr(hit), _ptr(t), _ptr(uv)))
+        return hit, t, uv
+
+    def close(self):
+        if self.handle:
+            lib().tpt_scene_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BVH:
+    """BVH (bvh.cuh:60-68): BVH(size) + construct(vertices, indices) -> m_nodes, m_keys.
+    Construction runs on the device (src/bvh.cu:304-331 semantics)."""
+
+    def __init__(self, size: int = 0):
+        self.size = size
+        self.m_nodes = np.zeros(max(2 * size - 1, 0), NODE_DTYPE)
+        self.m_keys = np.zeros(size, np.int64)
+
+    def construct(self, device_scene: DeviceScene):
+        if not device_scene.built:
+            device_scene.build()
+        self.m_nodes, self.m_keys = device_scene.read_bvh()
+        self.size = len(self.m_keys)
+        return self
+
+
+def procedural_sky(width=2048, height=1024):
+    """Deterministic equirect RGBA8 stand-in for the missing kloppenheim env
+    (SURVEY 8(d) C3).  Returns rows top-down (image order)."""
+    v = (np.arange(height, dtype=np.float64) + 0.5) / height          # 0 = top
+    u = (np.arange(width, dtype=np.float64) + 0.5) / width
+    theta = v * np.pi
+    phi = u * 2.0 * np.pi
+    elev = np.cos(theta)[:, None]
+    sky = np.clip(elev, 0.0, 1.0)
+    ground = np.clip(-elev, 0.0, 1.0)
+    sun = np.exp(-((theta[:, None] - 0.9) ** 2 + (np.cos(phi[None, :]) - 1.0) ** 2) * 40.0)
+    r = 0.45 + 0.25 * sky - 0.25 * ground + 0.5 * sun
+    g = 0.55 + 0.25 * sky - 0.30 * ground + 0.45 * sun
+    b = 0.75 + 0.20 * sky - 0.45 * ground + 0.30 * sun
+    img = np.stack([r + 0 * phi[None, :], g + 0 * phi[None, :], b + 0 * phi[None, :]], -1)
+    img = np.clip(img * 255.0, 0, 255).astype(np.uint8)
+    alpha = np.full((height, width, 1), 255, np.uint8)
+    return np.concatenate([img, alpha], -1)
+
+
+class EnvLight:
+    """EnvLight (env_light.cuh:8-18): equirect radiance, used on miss (A14).
+    Accepts an image file (PIL-readable, PFM/PPM) or an RGBA/RGB array in image
+    order (row 0 = top); stored row 0 = bottom like FreeImage (picture.h:41-43)."""
+
+    def __init__(self, source=None, device: int = 0):
+        self.device = device
+        self.handle = C.c_void_p()
+        if source is None or (isinstance(source, str) and source == ""):
+            self.rgba = None
+            return
+        if isinstance(source, str):
+            img = self._read(source)
+        else:
+            img = np.asarray(source, np.uint8)
+        if img.ndim != 3 or img.shape[2] not in (3, 4):
+            raise RuntimeError("Failed to create texture! Choose picture with 3 or 4 channels.")
+        if img.shape[2] == 3:
+            img = np.concatenate([img, np.full(img.shape[:2] + (1,), 255, np.uint8)], -1)
+        self.rgba = np.ascontiguousarray(img[::-1])           # bottom-up
+        h, w = self.rgba.shape[:2]
+        check(lib().tpt_env_create(_ptr(self.rgba), w, h, device, C.byref(self.handle)))
+
+    @staticmethod
+    def _read(path):
+        try:
+            from PIL import Image
+        except ImportError as e:   # pragma: no cover
+            raise RuntimeError(f"Failed to open file {path}: no image decoder") from e
+        try:
+            with Image.open(path) as im:
+                return np.asarray(im.convert("RGBA"))
+        except OSError as e:
+            raise RuntimeError(f"Failed to open file {path}") from e
+
+    def close(self):
+        if self.handle:
+            lib().tpt_env_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class Frame:
+    bgra: np.ndarray            # [H, W, 4] uint8, row 0 = top (copyToFB layout)
+    radiance: np.ndarray        # [H, W, 3] float32, row 0 = bottom (color / spp)
+    stats: dict = field(default_factory=dict)
+
+
+class PathTracer:
+    """PathTracer (include/path_tracer.h:16-35), headless.
+
+    The reference renders into a 1920x1080 Vulkan window forever, reseeding the
+    RNG with time() and drawing 64 spp per frame (path_tracer.cu:556-579).  Here
+    render() draws `frames` frames and returns the last one; seed=None keeps the
+    reference's time() seeding, an integer makes the frame reproducible."""
+
+    def __init__(self, envLightFile: str = "", width: int = 1920, height: int = 1080, device: int = 0):
+        self.m_width, self.m_height, self.device = width, height, device
+        self.envLight = EnvLight(envLightFile, device) if envLightFile else None
+
+    def doTrace(self, d_scene: DeviceScene, camera: Camera, framebuffer=None, nSamplesPerPixel: int = 64,
+                seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
+                flags: int = 0):
+        """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
+        or torch CUDA tensors / raw device pointers (device, int)."""
+        if not d_scene.built:
+            d_scene.build()
+        W, H = self.m_width, self.m_height
+        if seed is None:
+            seed = int(time.time())
+        p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags)
+        st = _lib.Stats()
+        env = self.envLight.handle if self.envLight is not None else None
+        rad_p = _addr(radiance)
+        fb_p = _addr(framebuffer)
+        cam = camera.to_c()
+        check(lib().tpt_render(d_scene.handle, env, C.byref(cam), C.byref(p), rad_p, fb_p, C.byref(st)))
+        return st.as_dict()
+
+    def render(self, meshFile: str, nSamplesPerPixel: int = 64, seed=None, max_depth: int = 8, frames: int = 1):
+        scene = Scene(meshFile, "gltf")
+        d_scene = scene.copySceneToDevice(self.device).build()
+        fb = np.zeros((self.m_height, self.m_width, 4), np.uint8)
+        fb[..., 3] = 255
+        rad = np.zeros((self.m_height, self.m_width, 3), np.float32)
+        stats = {}
+        for _ in range(frames):
+            stats = self.doTrace(d_scene, scene.m_camera, fb, nSamplesPerPixel, seed, max_depth, rad)
+        d_scene.close()
+        return Frame(fb, rad, stats)
+
+
+def _addr(buf):
+    if buf is None:
+        return None
+    if isinstance(buf, int):
+        return C.c_void_p(buf)
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            raise ValueError("output buffers must be contiguous")
+        return C.c_void_p(buf.ctypes.data)
+    if hasattr(buf, "data_ptr"):             # torch tensor (device memory)
+        if not buf.is_contiguous():
+            raise ValueError("output tensors must be contiguous")
+        return C.c_void_p(buf.data_ptr())
+    raise TypeError(f"unsupported buffer type {type(buf)}")

@@ -1,0 +1,122 @@
+// device_api.hpp -- launch entry points of the HIP kernels (host-callable).
+//
+// HBM layout of a built scene (see DESIGN.md "Data layout"):
+//   inner[4*(F-1)] float4  internal node i: both child AABBs + child links
+//       q0 = (L.min.xyz, L.max.x)  q1 = (L.max.yz, R.min.xy)
+//       q2 = (R.min.z, R.max.xyz)  q3 = (bits(left), bits(right), 0, 0)
+//     child ids use the reference numbering (bvh.cu:164-214): id >= F-1 is
+//     the leaf at sorted position id-(F-1).
+//   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
+//   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, 0), (n2.xyz, 0)
+//   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace tpt {
+
+struct DevLight {
+    int32_t type;
+    float color[3];
+    float intensity;
+    float pos[3];
+    float dir[3];
+    float cos_outer;
+    float inv_cos_cone_diff;
+};
+
+constexpr int kMaxLights = 16;
+constexpr int kRngJumps = 16;            // base-4 digits: up to 4^16 = 2^32 pixels
+constexpr int kJumpWords = 160 * 5;      // one 160x160 GF(2) matrix
+
+struct TraceArgs {
+    // scene
+    const float4* inner;
+    const float4* tri;
+    const float4* shade;
+    const float4* mtl;
+    int32_t n_faces;
+    int32_t n_materials;
+    int32_t n_lights;
+    int32_t stack_depth;                 // LDS stack slots per lane
+    const DevLight* lights;
+    // env (nullable)
+    const uint32_t* env;                 // RGBA8 packed, row 0 = bottom
+    int32_t env_w, env_h;
+    // camera
+    float c2w[16];
+    float origin[3];                     // c2w * (0,0,0,1)
+    float sensor_w, sensor_h;            // aspect*2tan(vfov/2), 2tan(vfov/2)
+    float half_sw, half_sh;              // 0.5*sensor_w, 0.5*sensor_h
+    float inv_w, inv_h;                  // 1/W, 1/H
+    // frame
+    int32_t width, height;
+    int32_t band_rows, band_count, band_index, band_height;   // band_height: rows in this band
+    int32_t max_depth;
+    int32_t samples;                     // samples for this launch
+    int32_t flags;
+    // per-pixel state (SoA over W*H pixels)
+    uint32_t* rng;                       // 6 planes: v0..v4, d
+    float* accum;                        // 3 planes: r, g, b (running totalRad)
+    unsigned long long* counters;        // [0] trav [1] inner [2] leaf [3] shade [4] overflow
+};
+
+struct ResolveArgs {
+    const float* accum;
+    float* radiance;                     // device, W*H*3 (nullable)
+    uint8_t* bgra;                       // device, W*H*4 (nullable)
+    int32_t width, height;
+    int32_t band_rows, band_count, band_index, band_height;
+    int32_t spp;
+};
+
+// rng.hip
+hipError_t launch_rng_init(const uint32_t* jumps, uint64_t seed, int32_t width, int32_t band_rows,
+                           int32_t band_count, int32_t band_index, int32_t band_height, int32_t height,
+                           uint32_t* rng, hipStream_t s);
+hipError_t launch_rng_init_linear(const uint32_t* jumps, uint64_t seed, uint64_t first, uint32_t n,
+                                  uint32_t* states_aos, hipStream_t s);
+
+// build.hip
+struct BuildBuffers {
+    int32_t n_faces, n_vertices, n_objects, n_materials;
+    const uint32_t* indices;
+    const float* vertices;
+    const float* normals;
+    const int2* lut;
+    const float* vert_trans;
+    const float* normal_trans;
+    const float4* mtl;
+    float* wverts;
+    float* wnorms;
+    // temporaries
+    unsigned long long* keys;
+    unsigned long long* keys_sorted;
+    uint32_t* fids;
+    uint32_t* fids_sorted;
+    float* leaf_box;                     // 6 per face (min.xyz, max.xyz) by fid
+    int2* children;                      // F-1
+    uint32_t* parent;                    // 2F-1
+    float* node_box;                     // 6 per node (2F-1)
+    uint32_t* flags;                     // F-1
+    uint32_t* max_depth;                 // 1
+    void* sort_tmp;
+    size_t sort_tmp_bytes;
+    // outputs
+    float4* inner;
+    float4* tri;
+    float4* shade;
+    void* nodes36;                       // reference layout (2F-1) * 36 B
+    uint32_t out_max_depth;              // deepest leaf (root = 0), set by launch_build
+};
+hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes);
+hipError_t launch_build(BuildBuffers& b, hipStream_t s);
+
+// trace.hip
+hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
+hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
+hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int32_t* hit,
+                             float* t, float* uv, hipStream_t s);
+
+}  // namespace tpt

@@ -1,0 +1,125 @@
+// ptrig.hpp -- double-precision sin/cos/atan2/acos for the parity-trig contract.
+//
+// The hot path needs (float) f((double) x) for the reference's fp32
+// transcendentals (tpt_math.hpp).  General-purpose double routines carry
+// large-argument reduction that costs many VGPRs; the arguments here are
+// bounded (phi = 2*pi*u in (0, 2*pi]; atan2/acos of unit-vector components),
+// so a two-constant Cody-Waite reduction plus fdlibm-style kernel polynomials
+// (error < 1 ulp of double) give the same float after rounding as the CPU
+// oracle's libm doubles, except when the double lies within ~2^-29 of a float
+// rounding boundary.  tests/test_cpu_math.py measures the agreement.
+#pragma once
+
+#include "tpt_math.hpp"
+
+namespace tpt {
+
+TPT_HD double dfma(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fma(a, b, c);
+#else
+    return std::fma(a, b, c);
+#endif
+}
+
+// sin and cos of x, |x| <= ~8 (phi in (0, 2*pi])
+TPT_HD void dsincos_small(double x, double& s, double& c) {
+    const double kInvPio2 = 6.36619772367581382433e-01;
+    const double kPio2_1 = 1.57079632673412561417e+00;    // first 33 bits of pi/2
+    const double kPio2_1t = 6.07710050650619224932e-11;   // pi/2 - kPio2_1
+    const double kd = rint(x * kInvPio2);
+    const int q = (int)kd & 3;
+    const double r = (x - kd * kPio2_1) - kd * kPio2_1t;
+    const double z = r * r;
+    // sin kernel (|r| <= pi/4)
+    double ps = dfma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    ps = dfma(z, ps, 2.75573137070700676789e-06);
+    ps = dfma(z, ps, -1.98412698298579493134e-04);
+    ps = dfma(z, ps, 8.33333333332248946124e-03);
+    ps = dfma(z, ps, -1.66666666666666324348e-01);
+    const double sr = dfma(r * z, ps, r);
+    // cos kernel
+    double pc = dfma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    pc = dfma(z, pc, -2.75573143513906633035e-07);
+    pc = dfma(z, pc, 2.48015872894767294178e-05);
+    pc = dfma(z, pc, -1.38888888888741095749e-03);
+    pc = dfma(z, pc, 4.16666666666666019037e-02);
+    const double hz = 0.5 * z;
+    const double w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * z * pc);
+    switch (q) {
+        case 0: s = sr; c = cr; break;
+        case 1: s = cr; c = -sr; break;
+        case 2: s = -sr; c = -cr; break;
+        default: s = -cr; c = sr; break;
+    }
+}
+
+// atan(t) for t >= 0 (fdlibm s_atan.c reduction + polynomial)
+TPT_HD double datan_pos(double t) {
+    double hi = 0.0, lo = 0.0;
+    int id;
+    if (t < 0.4375) {
+        id = -1;
+    } else if (t < 1.1875) {
+        if (t < 0.6875) { id = 0; t = (2.0 * t - 1.0) / (2.0 + t); }
+        else { id = 1; t = (t - 1.0) / (t + 1.0); }
+    } else if (t < 2.4375) {
+        id = 2; t = (t - 1.5) / (1.0 + 1.5 * t);
+    } else {
+        id = 3; t = -1.0 / t;
+    }
+    if (id == 0) { hi = 4.63647609000806093515e-01; lo = 2.26987774529616870924e-17; }
+    if (id == 1) { hi = 7.85398163397448278999e-01; lo = 3.06161699786838301793e-17; }
+    if (id == 2) { hi = 9.82793723247329054082e-01; lo = 1.39033110312309984516e-17; }
+    if (id == 3) { hi = 1.57079632679489655800e+00; lo = 6.12323399573676603587e-17; }
+    const double z = t * t;
+    const double w = z * z;
+    double s1 = dfma(w, 1.62858201153657823623e-02, 4.97687799461593236017e-02);
+    s1 = dfma(w, s1, 6.66107313738753120669e-02);
+    s1 = dfma(w, s1, 9.09088713343650656196e-02);
+    s1 = dfma(w, s1, 1.42857142725034663711e-01);
+    s1 = dfma(w, s1, 3.33333333333329318027e-01);
+    s1 = z * s1;
+    double s2 = dfma(w, -3.65315727442169155270e-02, -5.83357013379057348645e-02);
+    s2 = dfma(w, s2, -7.69187620504482999495e-02);
+    s2 = dfma(w, s2, -1.11111104054623557880e-01);
+    s2 = dfma(w, s2, -1.99999999998764832476e-01);
+    s2 = w * s2;
+    if (id < 0) return t - t * (s1 + s2);
+    return hi - ((t * (s1 + s2) - lo) - t);
+}
+
+TPT_HD double datan2(double y, double x) {
+    const double kPi = 3.1415926535897931160e+00, kPiLo = 1.2246467991473531772e-16;
+    if (x != x || y != y) return x + y;
+    const double ax = x < 0.0 ? -x : x, ay = y < 0.0 ? -y : y;
+    const bool yneg = __builtin_signbit(y);
+    if (ay == 0.0) {   // atan2(+-0, x): +-0 for x > 0 or +0, +-pi for x < 0 or -0
+        if (__builtin_signbit(x)) return yneg ? -kPi : kPi;
+        return y;
+    }
+    if (ax == 0.0) return yneg ? -1.57079632679489655800e+00 : 1.57079632679489655800e+00;
+    double a;
+    if (ax == ay && ax > 1.0e308) a = 7.85398163397448278999e-01;   // inf/inf
+    else a = datan_pos(ay / ax);
+    if (x < 0.0) a = (kPi - (a - kPiLo));
+    return yneg ? -a : a;
+}
+
+TPT_HD double dacos(double y) {
+    if (y != y || y > 1.0 || y < -1.0) return (y - y) / (y - y);
+    return datan2(sqrt((1.0 - y) * (1.0 + y)), y);
+}
+
+// Parity trig for the hot path (see tpt_math.hpp psin/pcos/...).
+TPT_HD void psincos2pi(float phi, float& s, float& c) {
+    double ds, dc;
+    dsincos_small((double)phi, ds, dc);
+    s = (float)ds;
+    c = (float)dc;
+}
+TPT_HD float patan2_fast(float y, float x) { return (float)datan2((double)y, (double)x); }
+TPT_HD float pacos_fast(float y) { return (float)dacos((double)y); }
+
+}  // namespace tpt

@@ -1,0 +1,597 @@
+// api.cpp -- the C-ABI (include/tpt.h) over the HIP kernels.
+//
+// Replaces the reference's per-frame orchestration PathTracer::doTrace
+// (src/path_tracer.cu:491-554) and Scene::copySceneToDevice (src/mesh.cu:309-397).
+// No exceptions cross the ABI: every entry point returns tpt_status and records
+// a thread-local message for tpt_last_error().
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../common/device_api.hpp"
+#include "../common/rng.hpp"
+#include "tpt.h"
+#include "tpt_internal.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+tpt_status fail(tpt_status st, const std::string& msg) {
+    g_last_error = msg;
+    return st;
+}
+
+#define HIP_OR_FAIL(expr)                                                                             \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail(e_ == hipErrorOutOfMemory ? TPT_ERR_OOM : TPT_ERR_HIP,                         \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                          \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t count) {
+        if (count == n && p) return hipSuccess;
+        release();
+        if (count == 0) return hipSuccess;
+        hipError_t e = hipMalloc((void**)&p, count * sizeof(T));
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+    hipError_t upload(const T* src, size_t count, hipStream_t s) {
+        hipError_t e = alloc(count);
+        if (e != hipSuccess || count == 0) return e;
+        return hipMemcpyAsync(p, src, count * sizeof(T), hipMemcpyHostToDevice, s);
+    }
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+std::vector<uint32_t>& host_jumps() {
+    static std::vector<uint32_t> j;
+    if (j.empty()) {
+        j.resize((size_t)tpt::kRngJumps * tpt::kJumpWords);
+        tpt::xorwow_jump_matrices(tpt::kRngJumps, j.data());
+    }
+    return j;
+}
+
+int band_height_of(int height, int band_rows, int band_count, int band_index) {
+    int n = 0;
+    for (int y = 0; y < height; ++y)
+        if ((y / band_rows) % band_count == band_index) ++n;
+    return n;
+}
+
+}  // namespace
+
+struct tpt_env {
+    int device = 0;
+    int w = 0, h = 0;
+    DevBuf<uint32_t> texels;
+};
+
+struct tpt_scene {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int32_t n_faces = 0, n_vertices = 0, n_objects = 0, n_materials = 0, n_lights = 0;
+    bool built = false;
+    int32_t stack_depth = 0;
+    uint32_t tree_depth = 0;
+    // inputs
+    DevBuf<uint32_t> indices;
+    DevBuf<float> vertices, normals, vert_trans, normal_trans;
+    DevBuf<int2> lut;
+    DevBuf<float4> mtl;
+    DevBuf<tpt::DevLight> lights;
+    DevBuf<uint32_t> jumps;
+    // world + BVH
+    DevBuf<float> wverts, wnorms, leaf_box, node_box;
+    DevBuf<unsigned long long> keys, keys_sorted;
+    DevBuf<uint32_t> fids, fids_sorted, parent, flags, max_depth;
+    DevBuf<int2> children;
+    DevBuf<uint8_t> sort_tmp, nodes36;
+    DevBuf<float4> inner, tri, shade;
+    // frame state
+    DevBuf<uint32_t> rng;
+    DevBuf<float> accum, radiance_tmp;
+    DevBuf<uint8_t> bgra_tmp;
+    DevBuf<unsigned long long> counters;
+    size_t frame_pixels = 0;
+
+    ~tpt_scene() {
+        DeviceGuard g(device);
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+extern "C" {
+
+const char* tpt_version(void) { return "tpt-mi355x 0.1 (gfx950)"; }
+
+const char* tpt_last_error(void) { return g_last_error.c_str(); }
+
+int tpt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+tpt_status tpt_scene_create(const tpt_scene_desc* d, int device, tpt_scene** out) {
+    if (!d || !out) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (d->n_faces == 0 || !d->indices || !d->vertices || !d->normals || d->n_vertices == 0)
+        return fail(TPT_ERR_INVALID_ARG, "scene needs faces, vertices and normals");
+    if (d->n_objects == 0 || !d->lut || !d->vert_trans || !d->normal_trans)
+        return fail(TPT_ERR_INVALID_ARG, "scene needs at least one object (LUT + transforms)");
+    if (d->n_lights > (uint32_t)tpt::kMaxLights) return fail(TPT_ERR_INVALID_ARG, "too many delta lights (max 16)");
+    if (d->n_faces > (1u << 30)) return fail(TPT_ERR_INVALID_ARG, "too many faces");
+    for (uint64_t i = 0; i < 3ull * d->n_faces; ++i)
+        if (d->indices[i] >= d->n_vertices) return fail(TPT_ERR_INVALID_ARG, "vertex index out of range");
+    if (d->lut[0].begin != 0) return fail(TPT_ERR_INVALID_ARG, "first object must begin at face 0");
+    int ndev = tpt_device_count();
+    if (ndev <= 0) return fail(TPT_ERR_NO_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(TPT_ERR_INVALID_ARG, "bad device index");
+
+    DeviceGuard g(device);
+    tpt_scene* s = new (std::nothrow) tpt_scene();
+    if (!s) return fail(TPT_ERR_OOM, "host allocation failed");
+    s->device = device;
+    auto cleanup = [&](tpt_status st) {
+        delete s;
+        return st;
+    };
+    hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+    for (int i = 0; e == hipSuccess && i < 4; ++i) e = hipEventCreate(&s->ev[i]);
+    if (e != hipSuccess) return cleanup(fail(TPT_ERR_HIP, std::string("stream/event: ") + hipGetErrorString(e)));
+
+    s->n_faces = (int32_t)d->n_faces;
+    s->n_vertices = (int32_t)d->n_vertices;
+    s->n_objects = (int32_t)d->n_objects;
+    s->n_materials = (int32_t)d->n_materials;
+    s->n_lights = (int32_t)d->n_lights;
+
+    std::vector<int2> lut(d->n_objects);
+    for (uint32_t i = 0; i < d->n_objects; ++i) lut[i] = make_int2(d->lut[i].begin, d->lut[i].mtl);
+    // materials + one Material() slot for meshes without a material (App. A.9)
+    std::vector<float4> mtl(2 * ((size_t)d->n_materials + 1));
+    for (uint32_t i = 0; i <= d->n_materials; ++i) {
+        tpt_material m = (i < d->n_materials && d->materials) ? d->materials[i] : tpt::default_material();
+        mtl[2 * i] = make_float4(m.base_color[0], m.base_color[1], m.base_color[2], m.emission_factor);
+        mtl[2 * i + 1] = make_float4(m.eta, m.metallic, 0.0f, 0.0f);
+    }
+    std::vector<tpt::DevLight> lights(d->n_lights);
+    for (uint32_t i = 0; i < d->n_lights; ++i) {
+        const tpt_light& L = d->lights[i];
+        tpt::DevLight& o = lights[i];
+        o.type = L.type;
+        std::memcpy(o.color, L.color, sizeof o.color);
+        o.intensity = L.intensity;
+        std::memcpy(o.pos, L.pos, sizeof o.pos);
+        std::memcpy(o.dir, L.direction, sizeof o.dir);
+        o.cos_outer = L.cos_outer;
+        o.inv_cos_cone_diff = L.inv_cos_cone_diff;
+    }
+    const auto& jumps = host_jumps();
+    hipStream_t st = s->stream;
+    e = s->indices.upload(d->indices, 3 * (size_t)d->n_faces, st);
+    if (e == hipSuccess) e = s->vertices.upload(d->vertices, 3 * (size_t)d->n_vertices, st);
+    if (e == hipSuccess) e = s->normals.upload(d->normals, 3 * (size_t)d->n_vertices, st);
+    if (e == hipSuccess) e = s->lut.upload(lut.data(), lut.size(), st);
+    if (e == hipSuccess) e = s->vert_trans.upload(d->vert_trans, 16 * (size_t)d->n_objects, st);
+    if (e == hipSuccess) e = s->normal_trans.upload(d->normal_trans, 16 * (size_t)d->n_objects, st);
+    if (e == hipSuccess) e = s->mtl.upload(mtl.data(), mtl.size(), st);
+    if (e == hipSuccess && !lights.empty()) e = s->lights.upload(lights.data(), lights.size(), st);
+    if (e == hipSuccess) e = s->jumps.upload(jumps.data(), jumps.size(), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess)
+        return cleanup(fail(e == hipErrorOutOfMemory ? TPT_ERR_OOM : TPT_ERR_HIP,
+                            std::string("scene upload: ") + hipGetErrorString(e)));
+    *out = s;
+    return TPT_OK;
+}
+
+tpt_status tpt_scene_build(tpt_scene* s) {
+    if (!s) return fail(TPT_ERR_INVALID_ARG, "null scene");
+    DeviceGuard g(s->device);
+    const size_t n = (size_t)s->n_faces, nn = 2 * n - 1, nv = (size_t)s->n_vertices;
+    size_t sort_bytes = 0;
+    HIP_OR_FAIL(tpt::build_sort_tmp_bytes((int32_t)n, &sort_bytes));
+    HIP_OR_FAIL(s->wverts.alloc(3 * nv));
+    HIP_OR_FAIL(s->wnorms.alloc(3 * nv));
+    HIP_OR_FAIL(hipMemsetAsync(s->wverts.p, 0, 3 * nv * sizeof(float), s->stream));
+    HIP_OR_FAIL(hipMemsetAsync(s->wnorms.p, 0, 3 * nv * sizeof(float), s->stream));
+    HIP_OR_FAIL(s->keys.alloc(n));
+    HIP_OR_FAIL(s->keys_sorted.alloc(n));
+    HIP_OR_FAIL(s->fids.alloc(n));
+    HIP_OR_FAIL(s->fids_sorted.alloc(n));
+    HIP_OR_FAIL(s->leaf_box.alloc(6 * n));
+    HIP_OR_FAIL(s->children.alloc(std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->parent.alloc(nn));
+    HIP_OR_FAIL(s->node_box.alloc(6 * nn));
+    HIP_OR_FAIL(s->flags.alloc(nn));
+    HIP_OR_FAIL(s->max_depth.alloc(1));
+    HIP_OR_FAIL(s->sort_tmp.alloc(std::max<size_t>(sort_bytes, 16)));
+    HIP_OR_FAIL(s->inner.alloc(4 * std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->tri.alloc(3 * n));
+    HIP_OR_FAIL(s->shade.alloc(3 * n));
+    HIP_OR_FAIL(s->nodes36.alloc(36 * nn));
+    HIP_OR_FAIL(hipMemsetAsync(s->parent.p, 0, nn * sizeof(uint32_t), s->stream));
+
+    tpt::BuildBuffers b{};
+    b.n_faces = s->n_faces;
+    b.n_vertices = s->n_vertices;
+    b.n_objects = s->n_objects;
+    b.n_materials = s->n_materials;
+    b.indices = s->indices.p;
+    b.vertices = s->vertices.p;
+    b.normals = s->normals.p;
+    b.lut = s->lut.p;
+    b.vert_trans = s->vert_trans.p;
+    b.normal_trans = s->normal_trans.p;
+    b.mtl = s->mtl.p;
+    b.wverts = s->wverts.p;
+    b.wnorms = s->wnorms.p;
+    b.keys = s->keys.p;
+    b.keys_sorted = s->keys_sorted.p;
+    b.fids = s->fids.p;
+    b.fids_sorted = s->fids_sorted.p;
+    b.leaf_box = s->leaf_box.p;
+    b.children = s->children.p;
+    b.parent = s->parent.p;
+    b.node_box = s->node_box.p;
+    b.flags = s->flags.p;
+    b.max_depth = s->max_depth.p;
+    b.sort_tmp = s->sort_tmp.p;
+    b.sort_tmp_bytes = sort_bytes;
+    b.inner = s->inner.p;
+    b.tri = s->tri.p;
+    b.shade = s->shade.p;
+    b.nodes36 = s->nodes36.p;
+    HIP_OR_FAIL(tpt::launch_build(b, s->stream));
+    s->tree_depth = b.out_max_depth;
+    // DFS that pushes both children holds at most depth + 1 entries
+    s->stack_depth = (int32_t)std::max<uint32_t>(b.out_max_depth + 2, 2);
+    if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
+    s->built = true;
+    return TPT_OK;
+}
+
+void tpt_scene_destroy(tpt_scene* s) { delete s; }
+
+tpt_status tpt_env_create(const uint8_t* rgba, int32_t w, int32_t h, int device, tpt_env** out) {
+    if (!rgba || !out || w <= 0 || h <= 0) return fail(TPT_ERR_INVALID_ARG, "bad env arguments");
+    *out = nullptr;
+    int ndev = tpt_device_count();
+    if (ndev <= 0) return fail(TPT_ERR_NO_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(TPT_ERR_INVALID_ARG, "bad device index");
+    DeviceGuard g(device);
+    tpt_env* env = new (std::nothrow) tpt_env();
+    if (!env) return fail(TPT_ERR_OOM, "host allocation failed");
+    env->device = device;
+    env->w = w;
+    env->h = h;
+    hipError_t e = env->texels.alloc((size_t)w * (size_t)h);
+    if (e == hipSuccess) e = hipMemcpy(env->texels.p, rgba, (size_t)w * h * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        delete env;
+        return fail(TPT_ERR_HIP, std::string("env upload: ") + hipGetErrorString(e));
+    }
+    *out = env;
+    return TPT_OK;
+}
+
+void tpt_env_destroy(tpt_env* env) {
+    if (!env) return;
+    DeviceGuard g(env->device);
+    delete env;
+}
+
+static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, tpt::TraceArgs& a) {
+    a.inner = s->inner.p;
+    a.tri = s->tri.p;
+    a.shade = s->shade.p;
+    a.mtl = s->mtl.p;
+    a.n_faces = s->n_faces;
+    a.n_materials = s->n_materials;
+    a.n_lights = s->n_lights;
+    a.lights = s->lights.p;
+    a.stack_depth = s->stack_depth;
+    a.env = env ? env->texels.p : nullptr;
+    a.env_w = env ? env->w : 0;
+    a.env_h = env ? env->h : 0;
+    if (cam) {
+        std::memcpy(a.c2w, cam->c2w, sizeof a.c2w);
+        float r[4];
+        tpt::mat4_vec4(cam->c2w, 0.0f, 0.0f, 0.0f, 1.0f, r);   // sampleRays :57
+        a.origin[0] = r[0];
+        a.origin[1] = r[1];
+        a.origin[2] = r[2];
+        const float tan_half = tpt::ptan(cam->vfov * 0.5f);    // :50-52
+        a.sensor_h = 2.0f * tan_half;
+        a.sensor_w = cam->aspect * a.sensor_h;
+        a.half_sw = 0.5f * a.sensor_w;
+        a.half_sh = 0.5f * a.sensor_h;
+    }
+    return TPT_OK;
+}
+
+tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, const tpt_params* p,
+                      float* radiance_out, uint8_t* bgra_out, tpt_stats* stats) {
+    auto t_start = std::chrono::steady_clock::now();
+    if (!s || !cam || !p) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    if (!s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built (call tpt_scene_build)");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 1 || p->max_depth > 64)
+        return fail(TPT_ERR_INVALID_ARG, "bad frame parameters");
+    if ((int64_t)p->width * p->height > (int64_t)1 << 30) return fail(TPT_ERR_INVALID_ARG, "frame too large");
+    const int band_count = p->band_count > 0 ? p->band_count : 1;
+    const int band_rows = p->band_rows > 0 ? p->band_rows : 16;
+    if (p->band_index < 0 || p->band_index >= band_count) return fail(TPT_ERR_INVALID_ARG, "bad band index");
+    if (env && env->device != s->device) return fail(TPT_ERR_INVALID_ARG, "env lives on another device");
+    DeviceGuard g(s->device);
+    hipStream_t st = s->stream;
+    const int W = p->width, H = p->height;
+    const size_t npix = (size_t)W * (size_t)H;
+    const int bh = band_height_of(H, band_rows, band_count, p->band_index);
+
+    HIP_OR_FAIL(s->rng.alloc(6 * npix));
+    HIP_OR_FAIL(s->accum.alloc(3 * npix));
+    HIP_OR_FAIL(s->counters.alloc(8));
+    HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * sizeof(float), st));   // thrust::fill (:534)
+    HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 8 * sizeof(unsigned long long), st));
+
+    // setupRandSeed (:513)
+    HIP_OR_FAIL(hipEventRecord(s->ev[0], st));
+    if (bh > 0)
+        HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, p->seed, W, band_rows, band_count, p->band_index, bh, H,
+                                         s->rng.p, st));
+    HIP_OR_FAIL(hipEventRecord(s->ev[1], st));
+
+    tpt::TraceArgs a{};
+    fill_trace_args(s, env, cam, a);
+    a.inv_w = 1.0f / (float)W;
+    a.inv_h = 1.0f / (float)H;
+    a.width = W;
+    a.height = H;
+    a.band_rows = band_rows;
+    a.band_count = band_count;
+    a.band_index = p->band_index;
+    a.band_height = bh;
+    a.max_depth = p->max_depth;
+    a.flags = p->flags;
+    a.rng = s->rng.p;
+    a.accum = s->accum.p;
+    a.counters = s->counters.p;
+
+    int chunk = p->spp_per_launch;
+    if (chunk <= 0) {
+        const double band_pix = (double)W * (double)std::max(bh, 1);
+        chunk = (int)std::max(1.0, std::floor(64.0 * 2073600.0 / band_pix));
+    }
+    chunk = std::min(chunk, p->spp);
+    double trace_ms = 0.0;
+    int launches = 0;
+    for (int done = 0; done < p->spp && bh > 0; done += chunk) {
+        a.samples = std::min(chunk, p->spp - done);
+        HIP_OR_FAIL(hipEventRecord(s->ev[2], st));
+        HIP_OR_FAIL(tpt::launch_trace(a, st));
+        HIP_OR_FAIL(hipEventRecord(s->ev[3], st));
+        HIP_OR_FAIL(hipEventSynchronize(s->ev[3]));
+        float ms = 0.0f;
+        HIP_OR_FAIL(hipEventElapsedTime(&ms, s->ev[2], s->ev[3]));
+        trace_ms += ms;
+        ++launches;
+    }
+
+    // copyToFB (:553) + radiance readout
+    const bool rad_dev = is_device_ptr(radiance_out);
+    const bool bgra_dev = is_device_ptr(bgra_out);
+    tpt::ResolveArgs r{};
+    r.accum = s->accum.p;
+    r.width = W;
+    r.height = H;
+    r.band_rows = band_rows;
+    r.band_count = band_count;
+    r.band_index = p->band_index;
+    r.band_height = bh;
+    r.spp = p->spp;
+    if (radiance_out) {
+        if (rad_dev) {
+            r.radiance = radiance_out;
+        } else {
+            HIP_OR_FAIL(s->radiance_tmp.alloc(3 * npix));
+            HIP_OR_FAIL(hipMemcpyAsync(s->radiance_tmp.p, radiance_out, 3 * npix * sizeof(float),
+                                       hipMemcpyHostToDevice, st));
+            r.radiance = s->radiance_tmp.p;
+        }
+    }
+    if (bgra_out) {
+        if (bgra_dev) {
+            r.bgra = bgra_out;
+        } else {
+            HIP_OR_FAIL(s->bgra_tmp.alloc(4 * npix));
+            HIP_OR_FAIL(hipMemcpyAsync(s->bgra_tmp.p, bgra_out, 4 * npix, hipMemcpyHostToDevice, st));
+            r.bgra = s->bgra_tmp.p;
+        }
+    }
+    HIP_OR_FAIL(hipEventRecord(s->ev[2], st));
+    if (bh > 0 && (r.radiance || r.bgra)) HIP_OR_FAIL(tpt::launch_resolve(r, st));
+    HIP_OR_FAIL(hipEventRecord(s->ev[3], st));
+    if (radiance_out && !rad_dev)
+        HIP_OR_FAIL(hipMemcpyAsync(radiance_out, s->radiance_tmp.p, 3 * npix * sizeof(float), hipMemcpyDeviceToHost,
+                                   st));
+    if (bgra_out && !bgra_dev)
+        HIP_OR_FAIL(hipMemcpyAsync(bgra_out, s->bgra_tmp.p, 4 * npix, hipMemcpyDeviceToHost, st));
+    unsigned long long cnt[8] = {0};
+    HIP_OR_FAIL(hipMemcpyAsync(cnt, s->counters.p, sizeof cnt, hipMemcpyDeviceToHost, st));
+    HIP_OR_FAIL(hipStreamSynchronize(st));
+    if (cnt[4] != 0) return fail(TPT_ERR_HIP, "traversal stack overflow (BVH deeper than sized)");
+    if (stats) {
+        std::memset(stats, 0, sizeof *stats);
+        stats->traversals = cnt[0];
+        stats->internal_visits = cnt[1];
+        stats->leaf_tests = cnt[2];
+        stats->shade_hits = cnt[3];
+        stats->pixels = (uint64_t)W * (uint64_t)bh;
+        stats->samples = stats->pixels * (uint64_t)p->spp;
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, s->ev[0], s->ev[1]);
+        stats->rng_init_ms = ms;
+        stats->trace_ms = trace_ms;
+        (void)hipEventElapsedTime(&ms, s->ev[2], s->ev[3]);
+        stats->resolve_ms = ms;
+        stats->trace_launches = launches;
+        stats->total_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    return TPT_OK;
+}
+
+tpt_status tpt_scene_read_bvh(tpt_scene* s, void* nodes36, int64_t* keys) {
+    if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
+    DeviceGuard g(s->device);
+    const size_t n = (size_t)s->n_faces;
+    if (nodes36) HIP_OR_FAIL(hipMemcpy(nodes36, s->nodes36.p, 36 * (2 * n - 1), hipMemcpyDeviceToHost));
+    if (keys) HIP_OR_FAIL(hipMemcpy(keys, s->keys_sorted.p, 8 * n, hipMemcpyDeviceToHost));
+    return TPT_OK;
+}
+
+tpt_status tpt_scene_read_world(tpt_scene* s, float* wv, float* wn) {
+    if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
+    DeviceGuard g(s->device);
+    const size_t nv = (size_t)s->n_vertices;
+    if (wv) HIP_OR_FAIL(hipMemcpy(wv, s->wverts.p, 12 * nv, hipMemcpyDeviceToHost));
+    if (wn) HIP_OR_FAIL(hipMemcpy(wn, s->wnorms.p, 12 * nv, hipMemcpyDeviceToHost));
+    return TPT_OK;
+}
+
+tpt_status tpt_debug_rng_init(int device, uint64_t seed, uint64_t first, uint32_t n, uint32_t* states) {
+    if (!states && n) return fail(TPT_ERR_INVALID_ARG, "null output");
+    int ndev = tpt_device_count();
+    if (ndev <= 0) return fail(TPT_ERR_NO_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(TPT_ERR_INVALID_ARG, "bad device index");
+    DeviceGuard g(device);
+    DevBuf<uint32_t> jumps, out;
+    const auto& hj = host_jumps();
+    HIP_OR_FAIL(jumps.upload(hj.data(), hj.size(), nullptr));
+    HIP_OR_FAIL(out.alloc(6 * (size_t)std::max(n, 1u)));
+    HIP_OR_FAIL(tpt::launch_rng_init_linear(jumps.p, seed, first, n, out.p, nullptr));
+    HIP_OR_FAIL(hipDeviceSynchronize());
+    if (n) HIP_OR_FAIL(hipMemcpy(states, out.p, 24 * (size_t)n, hipMemcpyDeviceToHost));
+    return TPT_OK;
+}
+
+tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const float* d, int32_t* hit, float* t,
+                                float* uv) {
+    if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
+    if (n && (!o || !d || !hit || !t || !uv)) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    DeviceGuard g(s->device);
+    DevBuf<float> dorg, ddir, dt, duv;
+    DevBuf<int32_t> dhit;
+    HIP_OR_FAIL(dorg.upload(o, 3 * (size_t)n, s->stream));
+    HIP_OR_FAIL(ddir.upload(d, 3 * (size_t)n, s->stream));
+    HIP_OR_FAIL(dhit.alloc(n));
+    HIP_OR_FAIL(dt.alloc(n));
+    HIP_OR_FAIL(duv.alloc(2 * (size_t)n));
+    tpt::TraceArgs a{};
+    fill_trace_args(s, nullptr, nullptr, a);
+    HIP_OR_FAIL(tpt::launch_trace_rays(a, n, dorg.p, ddir.p, dhit.p, dt.p, duv.p, s->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+    if (n) {
+        HIP_OR_FAIL(hipMemcpy(hit, dhit.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        HIP_OR_FAIL(hipMemcpy(t, dt.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        HIP_OR_FAIL(hipMemcpy(uv, duv.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    return TPT_OK;
+}
+
+tpt_status tpt_gltf_load(const char* path, tpt_gltf** out) {
+    if (!path || !out) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    tpt_gltf* g = new (std::nothrow) tpt_gltf();
+    if (!g) return fail(TPT_ERR_OOM, "host allocation failed");
+    try {
+        tpt::load_gltf(path, g->hs);
+    } catch (const tpt::io_error& e) {
+        delete g;
+        return fail(TPT_ERR_IO, e.what());
+    } catch (const std::exception& e) {
+        delete g;
+        return fail(TPT_ERR_PARSE, e.what());
+    }
+    *out = g;
+    return TPT_OK;
+}
+
+tpt_status tpt_gltf_desc(const tpt_gltf* g, tpt_scene_desc* d, tpt_camera* cam) {
+    if (!g || !d) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    const tpt::HostScene& h = g->hs;
+    d->indices = h.indices.data();
+    d->n_faces = (uint32_t)(h.indices.size() / 3);
+    d->vertices = h.vertices.data();
+    d->normals = h.normals.data();
+    d->n_vertices = (uint32_t)(h.vertices.size() / 3);
+    d->lut = h.lut.data();
+    d->n_objects = (uint32_t)h.lut.size();
+    d->vert_trans = h.vert_trans.data();
+    d->normal_trans = h.normal_trans.data();
+    d->materials = h.materials.empty() ? nullptr : h.materials.data();
+    d->n_materials = (uint32_t)h.materials.size();
+    d->lights = h.lights.empty() ? nullptr : h.lights.data();
+    d->n_lights = (uint32_t)h.lights.size();
+    if (cam) *cam = h.camera;
+    return TPT_OK;
+}
+
+int tpt_gltf_missing_material(const tpt_gltf* g) { return g && g->hs.missing_material ? 1 : 0; }
+
+void tpt_gltf_free(tpt_gltf* g) { delete g; }
+
+}  // extern "C"

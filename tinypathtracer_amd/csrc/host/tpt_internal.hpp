@@ -1,0 +1,49 @@
+// tpt_internal.hpp -- library internals shared by the host API and kernels.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "tpt.h"
+
+namespace tpt {
+
+struct io_error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct parse_error : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+// Material() defaults (include/material.h:88-103)
+inline tpt_material default_material() {
+    tpt_material m{};
+    m.base_color[0] = 0.82f; m.base_color[1] = 0.67f; m.base_color[2] = 0.16f;
+    m.emission_factor = 0.0f; m.eta = 0.0f; m.metallic = 0.0f; m.subsurface = 0.0f;
+    m.specular = 0.5f; m.roughness = 0.5f; m.specular_tint = 0.0f; m.anisotropic = 0.0f;
+    m.sheen = 0.0f; m.sheen_tint = 0.0f; m.clearcoat = 0.0f; m.clearcoat_gloss = 1.0f;
+    return m;
+}
+
+// Host scene produced by the glTF loader (the content of Scene + DeviceScene).
+struct HostScene {
+    std::vector<uint32_t> indices;
+    std::vector<float> vertices, normals;
+    std::vector<tpt_interval> lut;
+    std::vector<float> vert_trans, normal_trans;
+    std::vector<tpt_material> materials;
+    std::vector<tpt_light> lights;
+    tpt_camera camera{};
+    bool missing_material = false;
+};
+
+void load_gltf(const std::string& path, HostScene& hs);
+
+}  // namespace tpt
+
+struct tpt_gltf {
+    tpt::HostScene hs;
+};
