@@ -92,10 +92,12 @@ typedef struct {
     int32_t band_rows, band_count, band_index;
     int32_t spp_per_launch;       /* 0 = auto; chunks the spp loop over launches */
     int32_t flags;                /* TPT_FLAG_* */
+    int32_t refill;               /* 0 = auto: lanes (of 64) below which a wave stops to shade */
 } tpt_params;
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
 #define TPT_FLAG_REF_ORDER     0x2   /* reference right-first traversal, no culling */
+#define TPT_FLAG_LEGACY_LOOP   0x4   /* v2 loop: one whole traversal per lane per iteration */
 
 typedef struct {
     uint64_t traversals;          /* traverseBVH calls: primary+extension+probe+shadow */

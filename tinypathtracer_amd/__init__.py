@@ -283,7 +283,7 @@ class PathTracer:
 
     def doTrace(self, d_scene: DeviceScene, camera: Camera, framebuffer=None, nSamplesPerPixel: int = 64,
                 seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
-                flags: int = 0):
+                flags: int = 0, refill: int = 0):
         """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
         or torch CUDA tensors / raw device pointers (device, int)."""
         if not d_scene.built:
@@ -291,7 +291,8 @@ class PathTracer:
         W, H = self.m_width, self.m_height
         if seed is None:
             seed = int(time.time())
-        p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags)
+        p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags,
+                        refill)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
         rad_p = _addr(radiance)

@@ -16,6 +16,7 @@ TPT_OK = 0
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "HIP_ERROR", 3: "OOM", 4: "IO", 5: "PARSE", 6: "NO_DEVICE"}
 FLAG_NO_COUNTERS = 0x1
 FLAG_REF_ORDER = 0x2
+FLAG_LEGACY_LOOP = 0x4
 
 
 class Material(C.Structure):
@@ -52,7 +53,8 @@ class Camera(C.Structure):
 class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
                 ("seed", C.c_uint64), ("band_rows", C.c_int32), ("band_count", C.c_int32),
-                ("band_index", C.c_int32), ("spp_per_launch", C.c_int32), ("flags", C.c_int32)]
+                ("band_index", C.c_int32), ("spp_per_launch", C.c_int32), ("flags", C.c_int32),
+                ("refill", C.c_int32)]
 
 
 class Stats(C.Structure):

@@ -56,6 +56,7 @@ struct TraceArgs {
     int32_t max_depth;
     int32_t samples;                     // samples for this launch
     int32_t flags;
+    int32_t refill;                      // v3: leave the traversal loop below this many active lanes
     // per-pixel state (SoA over W*H pixels)
     uint32_t* rng;                       // 6 planes: v0..v4, d
     float* accum;                        // 3 planes: r, g, b (running totalRad)

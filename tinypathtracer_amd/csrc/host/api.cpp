@@ -406,6 +406,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     a.band_height = bh;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
+    a.refill = p->refill > 0 ? std::min(p->refill, 64) : 24;
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;

@@ -407,6 +407,277 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// v3 megakernel: ballot-driven traversal with postponed shading.
+//
+// A wave keeps stepping its lanes through BVH nodes while at least
+// `a.refill` of them are still traversing; once fewer are, it leaves the loop
+// and the finished lanes shade their hit, advance their path state machine and
+// set up their next ray (next bounce, shadow, probe or next sample), while the
+// unfinished lanes keep their traversal state (node, stack, best hit) in
+// registers and resume afterwards.  The wave therefore pays for the average
+// traversal length of its lanes instead of the longest one.
+// ---------------------------------------------------------------------------
+struct Trav {
+    V3 o, d, inv;
+    int node, sp, hpos, fid;
+    float t, u, v;
+    bool any_hit;
+};
+
+__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
+    r.o = o;
+    r.d = d;
+    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.node = 0;
+    r.sp = 0;
+    r.hpos = -1;
+    r.fid = -1;
+    r.t = kRealMax;
+    r.u = 0.0f;
+    r.v = 0.0f;
+    r.any_hit = any_hit;
+}
+
+// One node of traverseBVH (path_tracer.cu:61-107), same semantics as
+// traverse<ORDERED> above.  Returns false once the traversal has finished.
+template <bool ORDERED>
+__device__ __forceinline__ bool trav_step(Trav& r, const float4* __restrict__ inner, const float4* __restrict__ tri,
+                                          int nint, int* stk, int stack_depth, uint32_t& c_inner, uint32_t& c_leaf,
+                                          uint32_t& c_ovf) {
+    if (r.node < nint) {
+        ++c_inner;
+        const float4* nd = inner + 4 * r.node;
+        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        float l0, l1, r0, r1;
+        bool hl = box_hit(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
+        bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
+        const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
+        if (ORDERED) {
+            const float lim = r.t * 1.0001f;
+            hl = hl && !(l0 > lim) && !(l1 < 0.5f * kDelta);
+            hr = hr && !(r0 > lim) && !(r1 < 0.5f * kDelta);
+        }
+        if (hl && hr) {
+            int first = rc, second = lc;
+            if (ORDERED && l0 < r0) { first = lc; second = rc; }
+            if (r.sp >= stack_depth) { ++c_ovf; return false; }
+            stk[(r.sp++) * 256] = second;
+            r.node = first;
+            return true;
+        }
+        if (hl) { r.node = lc; return true; }
+        if (hr) { r.node = rc; return true; }
+    } else {
+        ++c_leaf;
+        const int pos = r.node - nint;
+        const float4* tr = tri + 3 * pos;
+        const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
+        const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
+        const V3 tv = r.o - v0;
+        const V3 p = cross(r.d, e2);
+        const V3 q = cross(tv, e1);
+        const float denom = dot(p, e1);
+        if (denom != 0.0f) {
+            const float id = 1.0f / denom;
+            const float u = dot(p, tv) * id;
+            const float v = dot(q, r.d) * id;
+            if (!(u < 0.0f || v < 0.0f || u + v > 1.0f)) {
+                const float t = dot(q, e2) * id;
+                const bool better = ORDERED ? (t < r.t || (t == r.t && r.hpos >= 0 && pos > r.hpos)) : (t < r.t);
+                if (better && t > kDelta) {
+                    r.t = t;
+                    r.fid = __float_as_int(q0.w);
+                    r.u = u;
+                    r.v = v;
+                    r.hpos = pos;
+                    if (r.any_hit) return false;
+                }
+            }
+        }
+    }
+    if (r.sp == 0) return false;
+    r.node = stk[(--r.sp) * 256];
+    return true;
+}
+
+enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2 };
+
+template <int MAXD, bool ORDERED>
+__global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
+    extern __shared__ int lds_stack[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
+    const bool active = x < a.width && ly < a.band_height && y < a.height;
+    uint32_t c_trav = 0, c_inner = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
+    const size_t npix = (size_t)a.width * (size_t)a.height;
+    const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
+    const int nint = a.n_faces - 1;
+    int* stk = lds_stack + tid;
+
+    uint32_t st[6];
+    V3 total = v3(0.0f, 0.0f, 0.0f);
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) st[i] = a.rng[i * npix + off];
+        total = v3(a.accum[off], a.accum[npix + off], a.accum[2 * npix + off]);
+    }
+    PathRecords<MAXD> rec;
+    int remaining = a.samples;
+    int phase = PH_CAMERA;
+    int depth = 0, li = 0, mtl = 0;
+    V3 rd = v3(0.0f, 0.0f, 0.0f), nd = rd, nrm = rd, direct = rd;
+    Trav r;
+    trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), false);
+    int ts = active ? TS_DONE : TS_DEAD;
+    const int refill = a.refill;
+
+    for (;;) {
+        if (ts == TS_DONE) {
+            // ---- consume the finished traversal (none for a fresh sample) ----
+            bool finish = false, lights_next = false, after = false;
+            V3 L = v3(0.0f, 0.0f, 0.0f);
+            if (phase == PH_EXT) {
+                if (r.fid < 0) {
+                    if (a.env) L = env_lookup(a.env, a.env_w, a.env_h, rd);
+                    finish = true;
+                } else {
+                    ++c_shade;
+                    const float4* sh = a.shade + 3 * r.fid;
+                    const float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
+                    const float w = 1.0f - r.u - r.v;
+                    nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (r.u * v3(s1.x, s1.y, s1.z))) +
+                                    (r.v * v3(s2.x, s2.y, s2.z)));
+                    r.o = r.o + (r.t * rd);
+                    mtl = __float_as_int(s0.w);
+                    const float4 m0 = a.mtl[2 * mtl], m1 = a.mtl[2 * mtl + 1];
+                    float af;
+                    const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
+                    rec.att[depth] = af * v3(m0.x, m0.y, m0.z);
+                    rec.ivp[depth] = 1.0f / prob;
+                    direct = v3(0.0f, 0.0f, 0.0f);
+                    li = 0;
+                    lights_next = true;
+                }
+            } else if (phase == PH_SHADOW) {
+                if (r.fid < 0) {   // sampleDeltaLights :279-282 (light re-sampled: deterministic)
+                    V3 ldir, lrad;
+                    light_sample(a.lights, li, r.o, ldir, lrad);
+                    const float4 m0 = a.mtl[2 * mtl];
+                    direct = direct + (v3(m0.x, m0.y, m0.z) * lrad);
+                }
+                ++li;
+                lights_next = true;
+            } else if (phase == PH_PROBE) {   // :390-400
+                V3 dl = direct;
+                if (r.fid >= 0) {
+                    const int pm = __float_as_int(a.shade[3 * r.fid].w);
+                    const float e = a.mtl[2 * pm].w;
+                    dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + direct;
+                }
+                rec.dst[depth] = dl;
+                after = true;
+            }
+            V3 td = rd;
+            bool shadow = false;
+            if (lights_next) {
+                const float4 m1 = a.mtl[2 * mtl + 1];
+                if (li < a.n_lights) {
+                    V3 lrad;
+                    light_sample(a.lights, li, r.o, td, lrad);
+                    phase = PH_SHADOW;
+                    shadow = true;
+                } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
+                    float af2;
+                    new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
+                    phase = PH_PROBE;
+                } else {
+                    rec.dst[depth] = direct;
+                    after = true;
+                }
+            }
+            if (after) {
+                const float e = a.mtl[2 * mtl].w;
+                if (e > 0.0f) {   // an emitter ends the path (:408-412); the unwind starts from e
+                    L = e * v3(1.0f, 1.0f, 1.0f);
+                    finish = true;
+                } else {
+                    rd = nd;
+                    td = rd;
+                    ++depth;
+                    if (depth == a.max_depth) finish = true;
+                    else phase = PH_EXT;
+                }
+            }
+            if (finish) {   // unwind (:416-431): levels depth-1 .. 0
+                for (int k = depth - 1; k >= 0; --k) L = rec.ivp[k] * ((rec.dst[k] + L) * rec.att[k]);
+                total = total + L;
+                phase = PH_CAMERA;
+            }
+            V3 to = r.o;
+            if (phase == PH_CAMERA) {
+                if (remaining == 0) {
+                    ts = TS_DEAD;
+                } else {
+                    --remaining;
+                    // sampleRays (path_tracer.cu:42-59)
+                    const float ju = xorwow_uniform(st);
+                    const float jv = xorwow_uniform(st);
+                    float lx = ju * 1.0f, lyf = jv * 1.0f;
+                    lx = lx + (float)x;
+                    lyf = lyf + (float)y;
+                    lx = lx * a.inv_w;
+                    lyf = lyf * a.inv_h;
+                    lx = lx * a.sensor_w;
+                    lyf = lyf * a.sensor_h;
+                    float r4[4];
+                    mat4_vec4(a.c2w, lx - a.half_sw, lyf - a.half_sh, 0.0f - 1.0f, 0.0f, r4);
+                    rd = normalize(v3(r4[0], r4[1], r4[2]));
+                    td = rd;
+                    to = v3(a.origin[0], a.origin[1], a.origin[2]);
+                    depth = 0;
+                    phase = PH_EXT;
+                }
+            }
+            if (ts != TS_DEAD) {
+                ++c_trav;
+                trav_begin(r, to, td, shadow);
+                ts = TS_TRAV;
+            }
+        }
+        if (__ballot(ts != TS_DEAD) == 0ull) break;
+        // ---- traversal: step while enough lanes of the wave are still traversing ----
+        for (;;) {
+            const unsigned long long tm = __ballot(ts == TS_TRAV);
+            const int cnt = __popcll(tm);
+            if (cnt == 0) break;
+            if (cnt < refill && __ballot(ts == TS_DONE) != 0ull) break;
+            if (ts == TS_TRAV) {
+                if (!trav_step<ORDERED>(r, a.inner, a.tri, nint, stk, a.stack_depth, c_inner, c_leaf, c_ovf))
+                    ts = TS_DONE;
+            }
+        }
+    }
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) a.rng[i * npix + off] = st[i];
+        a.accum[off] = total.x;
+        a.accum[npix + off] = total.y;
+        a.accum[2 * npix + off] = total.z;
+    }
+    const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
+                             s_shade = wave_sum(c_shade), s_ovf = wave_sum(c_ovf);
+    if (lane == 0) {
+        atomicAdd(&a.counters[0], s_trav);
+        atomicAdd(&a.counters[1], s_inner);
+        atomicAdd(&a.counters[2], s_leaf);
+        atomicAdd(&a.counters[3], s_shade);
+        if (s_ovf) atomicAdd(&a.counters[4], s_ovf);
+    }
+}
+
 // copyToFB (path_tracer.cu:451-471) + the radiance readout (color / spp).
 __global__ void k_resolve(ResolveArgs a) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -449,8 +720,19 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
     }
 }
 
-template <bool ORDERED>
+template <bool ORDERED, bool V3K>
 static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (V3K) {
+        if (a.max_depth <= 8)
+            hipLaunchKernelGGL((k_trace3<8, ORDERED>), grid, dim3(256), lds, s, a);
+        else if (a.max_depth <= 16)
+            hipLaunchKernelGGL((k_trace3<16, ORDERED>), grid, dim3(256), lds, s, a);
+        else if (a.max_depth <= 32)
+            hipLaunchKernelGGL((k_trace3<32, ORDERED>), grid, dim3(256), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_trace3<64, ORDERED>), grid, dim3(256), lds, s, a);
+        return;
+    }
     if (a.max_depth <= 8)
         hipLaunchKernelGGL((k_trace<8, ORDERED>), grid, dim3(256), lds, s, a);
     else if (a.max_depth <= 16)
@@ -464,10 +746,14 @@ static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s) {
     dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
     const size_t lds = (size_t)a.stack_depth * 256 * sizeof(int);
-    if (a.flags & TPT_FLAG_REF_ORDER)
-        launch_trace_t<false>(a, grid, lds, s);
-    else
-        launch_trace_t<true>(a, grid, lds, s);
+    const bool legacy = (a.flags & TPT_FLAG_LEGACY_LOOP) != 0;
+    if (a.flags & TPT_FLAG_REF_ORDER) {
+        if (legacy) launch_trace_t<false, false>(a, grid, lds, s);
+        else launch_trace_t<false, true>(a, grid, lds, s);
+    } else {
+        if (legacy) launch_trace_t<true, false>(a, grid, lds, s);
+        else launch_trace_t<true, true>(a, grid, lds, s);
+    }
     return hipGetLastError();
 }
 

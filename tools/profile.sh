@@ -1,0 +1,22 @@
+#!/bin/bash
+# rocprofv3 evidence for the trace kernel: kernel-trace stats + separate PMC passes
+# (never combined with sys/runtime tracing).  Usage: bash tools/profile.sh TAG [bench args]
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-r01}; shift
+ARGS=${@:---spp 64 --steps 1 --warmup 0 --cpu-baseline 0}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/ktrace.log 2>&1 || exit 1
+i=0
+while read -r PASS; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $PASS -d $OUT/pmc$i -o run --output-format csv -- python3 bench.py $ARGS > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+done <<'PASSES'
+SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_BRANCH
+TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
+FETCH_SIZE
+WRITE_SIZE
+PASSES
+python3 tools/pmc_summary.py $OUT > $OUT/summary.json && cat $OUT/summary.json
