@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--spp-per-launch", type=int, default=0)
-    ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference order, 4 = v2 loop)")
+    ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
     ap.add_argument("--refill", type=int, default=0, help="0 = library default")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port on rank 0 at N=1")
     ap.add_argument("--cpu-spp", type=int, default=16)

@@ -97,7 +97,6 @@ typedef struct {
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
 #define TPT_FLAG_REF_ORDER     0x2   /* reference right-first traversal, no culling */
-#define TPT_FLAG_LEGACY_LOOP   0x4   /* v2 loop: one whole traversal per lane per iteration */
 
 typedef struct {
     uint64_t traversals;          /* traverseBVH calls: primary+extension+probe+shadow */

@@ -73,12 +73,49 @@ static inline void mat4_vec4(const float* m, const float v[4], float r[4]) {
 
 /* ------------------------------------------------------------------------ */
 /* Transcendentals.  trig_mode 0: libm float (the survey's host harness);     */
-/* trig_mode 1: (float)f((double)x) -- evaluated identically by the HIP kernel */
+/* trig_mode 1: the HIP kernel's parity trig (ptrig.hpp): fp32 sincos below,  */
+/* (float)f((double)x) for atan2/acos/tan                                     */
 /* ------------------------------------------------------------------------ */
 float orc_parity_sinf(float x) { return (float)sin((double)x); }
 float orc_parity_cosf(float x) { return (float)cos((double)x); }
-static inline float t_sin(int m, float x) { return m ? (float)sin((double)x) : sinf(x); }
-static inline float t_cos(int m, float x) { return m ? (float)cos((double)x) : cosf(x); }
+/* fsincos_2pi: the HIP kernel's fp32 sin/cos of phi in [0, 2pi]
+ * (tinypathtracer_amd/csrc/common/ptrig.hpp) restated step for step: Cody-Waite
+ * reduction by pi/2 in three fmaf steps, minimax polynomials, quadrant swap. */
+static void parity_sincos(float x, float* s, float* c) {
+    const float k = rintf(x * 0.636619772f);
+    const int q = (int)k & 3;
+    float r = fmaf(-k, 1.57079637f, x);
+    r = fmaf(-k, -4.37113883e-08f, r);
+    r = fmaf(-k, -1.71512489e-15f, r);
+    const float z = r * r;
+    float ps = fmaf(z, 2.71808875e-06f, -1.98393362e-04f);
+    ps = fmaf(z, ps, 8.33332464e-03f);
+    ps = fmaf(z, ps, -1.66666657e-01f);
+    const float sr = fmaf(r * z, ps, r);
+    float pc = fmaf(z, 2.43904487e-05f, -1.38867637e-03f);
+    pc = fmaf(z, pc, 4.16666418e-02f);
+    pc = fmaf(z, pc, -0.5f);
+    const float cr = fmaf(z, pc, 1.0f);
+    switch (q) {
+        case 0: *s = sr; *c = cr; break;
+        case 1: *s = cr; *c = -sr; break;
+        case 2: *s = -sr; *c = -cr; break;
+        default: *s = -cr; *c = sr; break;
+    }
+}
+void orc_parity_sincos(float x, float* s, float* c) { parity_sincos(x, s, c); }
+static inline float t_sin(int m, float x) {
+    if (!m) return sinf(x);
+    float s, c;
+    parity_sincos(x, &s, &c);
+    return s;
+}
+static inline float t_cos(int m, float x) {
+    if (!m) return cosf(x);
+    float s, c;
+    parity_sincos(x, &s, &c);
+    return c;
+}
 static inline float t_acos(int m, float x) { return m ? (float)acos((double)x) : acosf(x); }
 static inline float t_atan2(int m, float y, float x) {
     return m ? (float)atan2((double)y, (double)x) : atan2f(y, x);

@@ -82,7 +82,7 @@ typedef struct {
     /* interleaved row bands: rows y with (y / band_rows) % band_count == band_index */
     int32_t band_rows, band_count, band_index;
     int32_t trig_mode;    /* 0: libm float functions (as the survey harness);
-                             1: parity trig (float)f((double)x), as the HIP kernel */
+                             1: parity trig, bit-identical to the HIP kernel */
     int32_t threads;      /* OpenMP threads, 0 = default */
 } orc_params;
 
@@ -124,6 +124,8 @@ int orc_trace_ray(const orc_node* nodes, uint32_t n_faces, const float* wverts,
 
 float orc_parity_sinf(float x);
 float orc_parity_cosf(float x);
+/* trig_mode 1 sin/cos of phi in [0, 2pi] (identical to the HIP kernel) */
+void orc_parity_sincos(float x, float* s, float* c);
 
 #ifdef __cplusplus
 }

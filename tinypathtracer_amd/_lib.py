@@ -16,7 +16,6 @@ TPT_OK = 0
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "HIP_ERROR", 3: "OOM", 4: "IO", 5: "PARSE", 6: "NO_DEVICE"}
 FLAG_NO_COUNTERS = 0x1
 FLAG_REF_ORDER = 0x2
-FLAG_LEGACY_LOOP = 0x4
 
 
 class Material(C.Structure):

@@ -1,13 +1,14 @@
-// ptrig.hpp -- double-precision sin/cos/atan2/acos for the parity-trig contract.
+// ptrig.hpp -- the transcendentals of the hot path ("parity trig").
 //
-// The hot path needs (float) f((double) x) for the reference's fp32
-// transcendentals (tpt_math.hpp).  General-purpose double routines carry
-// large-argument reduction that costs many VGPRs; the arguments here are
-// bounded (phi = 2*pi*u in (0, 2*pi]; atan2/acos of unit-vector components),
-// so a two-constant Cody-Waite reduction plus fdlibm-style kernel polynomials
-// (error < 1 ulp of double) give the same float after rounding as the CPU
-// oracle's libm doubles, except when the double lies within ~2^-29 of a float
-// rounding boundary.  tests/test_cpu_math.py measures the agreement.
+// The reference calls CUDA's fp32 sinf/cosf/atan2f/acosf (<= 2 ulp, not
+// reproducible off NVIDIA hardware).  This build fixes one evaluation that the
+// HIP kernel and the CPU oracle (trig_mode 1) perform bit-identically:
+//  * sin/cos of the diffuse sampler's phi (per bounce, hot): fsincos_2pi, an
+//    all-fp32 Cody-Waite + minimax evaluation with explicit fmaf, <= 1 ulp;
+//  * atan2/acos of the env lookup (cold): (float) of a double evaluation
+//    (fdlibm-style kernels below, < 1 ulp of double), which equals the oracle's
+//    (float)atan2((double)..) from libm except within ~2^-29 of a float
+//    rounding boundary.  tests/test_cpu_math.py measures both.
 #pragma once
 
 #include "tpt_math.hpp"
@@ -110,6 +111,43 @@ TPT_HD double datan2(double y, double x) {
 TPT_HD double dacos(double y) {
     if (y != y || y > 1.0 || y < -1.0) return (y - y) / (y - y);
     return datan2(sqrt((1.0 - y) * (1.0 + y)), y);
+}
+
+TPT_HD float ffma(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_fmaf(a, b, c);
+#else
+    return std::fma(a, b, c);
+#endif
+}
+
+// fp32 sin and cos of x in [0, 2*pi] (the diffuse sampler's phi = 2*pi*u,
+// sampler.h:81).  Cody-Waite reduction by pi/2 in three parts and minimax
+// polynomials on [-pi/4, pi/4]; every step is an explicit, correctly rounded
+// fmaf / mul / add, so the CPU oracle (trig_mode 1, tpt_oracle.c) evaluates the
+// very same bits.  Max error <= 1 ulp against the correctly rounded sin/cos
+// (tests/test_cpu_math.py), the accuracy class of CUDA's sinf/cosf.
+TPT_HD void fsincos_2pi(float x, float& s, float& c) {
+    const float k = rintf(x * 0.636619772f);
+    const int q = (int)k & 3;
+    float r = ffma(-k, 1.57079637f, x);          // pi/2 = 1.57079637 - 4.37113883e-8 + ...
+    r = ffma(-k, -4.37113883e-08f, r);
+    r = ffma(-k, -1.71512489e-15f, r);
+    const float z = r * r;
+    float ps = ffma(z, 2.71808875e-06f, -1.98393362e-04f);
+    ps = ffma(z, ps, 8.33332464e-03f);
+    ps = ffma(z, ps, -1.66666657e-01f);
+    const float sr = ffma(r * z, ps, r);
+    float pc = ffma(z, 2.43904487e-05f, -1.38867637e-03f);
+    pc = ffma(z, pc, 4.16666418e-02f);
+    pc = ffma(z, pc, -0.5f);
+    const float cr = ffma(z, pc, 1.0f);
+    switch (q) {
+        case 0: s = sr; c = cr; break;
+        case 1: s = cr; c = -sr; break;
+        case 2: s = -sr; c = -cr; break;
+        default: s = -cr; c = sr; break;
+    }
 }
 
 // Parity trig for the hot path (see tpt_math.hpp psin/pcos/...).

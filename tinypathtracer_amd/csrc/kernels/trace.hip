@@ -4,138 +4,168 @@
 // MI355X design (DESIGN.md "Trace kernel"):
 //  * one lane per pixel, 16x16 pixel tile per 256-thread workgroup, each wave an
 //    8x8 sub-tile (coherent primary rays);
-//  * the reference's nested spp -> depth -> {extension, shadow*, probe} loops are
-//    flattened into a per-lane state machine that issues exactly ONE BVH
-//    traversal per iteration from a single call site.  A lane whose path ends
-//    immediately regenerates its next sample, so a wave stays full across
-//    samples and bounces while every pixel still consumes its own XORWOW stream
-//    in the reference's order;
-//  * the traversal stack lives in LDS, [slot][lane] (conflict-free, sized to the
-//    built tree's depth); the per-depth path records (attenuation, 1/p, direct)
-//    are private arrays; RNG state and the running total live in registers and
-//    are persisted to HBM (SoA) between spp chunks;
+//  * the reference's nested spp -> depth -> {extension, shadow*, probe} loops
+//    become a per-lane state machine; every ray (primary, extension, shadow,
+//    probe) is one traversal that the wave steps node by node;
+//  * ballot-driven postponed shading: a wave keeps stepping while at least
+//    `refill` of its lanes are still traversing, then the finished lanes shade,
+//    advance their path and set up their next ray while the others keep their
+//    traversal state in registers -- the wave pays the average traversal length
+//    of its lanes, not the longest, and every pixel still consumes its own
+//    XORWOW stream in the reference's order;
+//  * LDS per lane: the traversal stack ([slot][lane], 16-bit node ids when the
+//    tree allows) and the path records of the first two bounces; deeper records
+//    spill to private memory (rare);
 //  * node records are 64 B (both child AABBs + links: one visit = four 16-B
 //    loads), triangles are pre-gathered (v0, e1, e2, fid: three 16-B loads).
 #include <hip/hip_runtime.h>
 
 #include "../common/device_api.hpp"
-#include "../common/rng.hpp"
 #include "../common/ptrig.hpp"
+#include "../common/rng.hpp"
 #include "../common/tpt_math.hpp"
 #include "tpt.h"
 
+#ifndef TPT_TRACE_WAVES
+#define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator
+#endif
+
 namespace tpt {
 
-struct Hit {
-    int fid;
-    float t, u, v;
-};
-
-// rayHitBBox (geometry_queries.h:18-46) with 1/dir hoisted per ray (same values).
-// Returns the reference's hit/miss verdict and the slab interval [t0, t1] for
-// the ordered traversal (NaN slabs propagate exactly as in the reference).
+// rayHitBBox (geometry_queries.h:18-46) with 1/dir hoisted per ray (same
+// values), written without branches: the reference returns false at the first
+// axis whose slab misses the running interval; a sticky `miss` flag gives the
+// same verdict (later axes cannot undo it) and the interval [t0, t1] -- used
+// only by the ordered traversal, only on a hit -- is the reference's sequence
+// of max/min updates.  NaN slabs propagate exactly as in the reference.
 __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, float ny, float nz, float xx,
                                         float xy, float xz, float& t0, float& t1) {
-    float a, b, s;
+    bool miss;
+    float a, b, lo, hi;
     t0 = -kRealMax;
     t1 = kRealMax;
     a = (nx - o.x) * inv.x;
     b = (xx - o.x) * inv.x;
-    if (a > b) { s = b; b = a; a = s; }
-    if (t0 > b || a > t1) return false;
-    t0 = fmx(t0, a);
-    t1 = fmn(t1, b);
+    lo = a > b ? b : a;
+    hi = a > b ? a : b;
+    miss = (t0 > hi) | (lo > t1);
+    t0 = fmx(t0, lo);
+    t1 = fmn(t1, hi);
     a = (ny - o.y) * inv.y;
     b = (xy - o.y) * inv.y;
-    if (a > b) { s = b; b = a; a = s; }
-    if (t0 > b || a > t1) return false;
-    t0 = fmx(t0, a);
-    t1 = fmn(t1, b);
+    lo = a > b ? b : a;
+    hi = a > b ? a : b;
+    miss = miss | (t0 > hi) | (lo > t1);
+    t0 = fmx(t0, lo);
+    t1 = fmn(t1, hi);
     a = (nz - o.z) * inv.z;
     b = (xz - o.z) * inv.z;
-    if (a > b) { s = b; b = a; a = s; }
-    if (t0 > b || a > t1) return false;
-    t0 = fmx(t0, a);
-    t1 = fmn(t1, b);
-    return true;
+    lo = a > b ? b : a;
+    hi = a > b ? a : b;
+    miss = miss | (t0 > hi) | (lo > t1);
+    t0 = fmx(t0, lo);
+    t1 = fmn(t1, hi);
+    return !miss;
 }
 
-// traverseBVH (path_tracer.cu:61-107).  The current node stays in a register;
-// the LDS stack ([slot][lane]) only holds deferred siblings.
-//  ORDERED == false: the reference's order exactly (both children hit -> the
-//    right child first, left deferred) -- same visit sequence as :95-104.
-//  ORDERED == true: nearer child first and a child is skipped when its slab
-//    entry lies beyond the best hit (with a 1e-4 relative margin) or its exit
-//    lies before Delta/2: boxes that cannot hold an accepted hit.  Exact ties
-//    (t == best) resolve to the larger leaf position, which is the triangle the
-//    reference's right-first DFS finds first, so the winner is the reference's.
-// any_hit: shadow rays stop at the first accepted triangle (only hitIdx == -1
-// matters, :279).
-template <bool ORDERED>
-__device__ __forceinline__ Hit traverse(const float4* __restrict__ inner, const float4* __restrict__ tri, int nint,
-                                        int* stk, int stack_depth, V3 o, V3 d, bool any_hit, uint32_t& c_inner,
-                                        uint32_t& c_leaf, uint32_t& c_ovf) {
-    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    Hit h{-1, kRealMax, 0.0f, 0.0f};
-    int hpos = -1;
-    int sp = 0;
-    int node = 0;
-    for (;;) {
-        if (node < nint) {
-            ++c_inner;
-            const float4* nd = inner + 4 * node;
-            const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-            float l0, l1, r0, r1;
-            bool hl = box_hit(o, inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
-            bool hr = box_hit(o, inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
-            const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
-            if (ORDERED) {
-                const float lim = h.t * 1.0001f;
-                hl = hl && !(l0 > lim) && !(l1 < 0.5f * kDelta);
-                hr = hr && !(r0 > lim) && !(r1 < 0.5f * kDelta);
-            }
-            if (hl && hr) {
-                int first = rc, second = lc;
-                if (ORDERED && l0 < r0) { first = lc; second = rc; }
-                if (sp >= stack_depth) { ++c_ovf; break; }
-                stk[(sp++) * 256] = second;
-                node = first;
-                continue;
-            }
-            if (hl) { node = lc; continue; }
-            if (hr) { node = rc; continue; }
-        } else {
-            ++c_leaf;
-            const int pos = node - nint;
-            const float4* tr = tri + 3 * pos;
-            const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
-            const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
-            const V3 tv = o - v0;
-            const V3 p = cross(d, e2);
-            const V3 q = cross(tv, e1);
-            const float denom = dot(p, e1);
-            if (denom != 0.0f) {
-                const float id = 1.0f / denom;
-                const float u = dot(p, tv) * id;
-                const float v = dot(q, d) * id;
-                if (!(u < 0.0f || v < 0.0f || u + v > 1.0f)) {
-                    const float t = dot(q, e2) * id;
-                    const bool better = ORDERED ? (t < h.t || (t == h.t && hpos >= 0 && pos > hpos)) : (t < h.t);
-                    if (better && t > kDelta) {
-                        h.t = t;
-                        h.fid = __float_as_int(q0.w);
-                        h.u = u;
-                        h.v = v;
-                        hpos = pos;
-                        if (any_hit) break;
-                    }
-                }
-            }
+// ---------------------------------------------------------------------------
+// Traversal (traverseBVH, path_tracer.cu:61-107), one node per step.  The
+// current node is in a register; the LDS stack only holds deferred siblings.
+//  ORDERED == false: the reference's visit order exactly (both children hit ->
+//    right first, left deferred: :95-104), no culling.
+//  ORDERED == true (default): nearer child first; a child is skipped when its
+//    slab entry lies beyond the best hit (1e-4 relative margin) or its exit lies
+//    before Delta/2 -- boxes that cannot hold an accepted hit.  Exact ties
+//    (t == best) resolve to the larger leaf position, the triangle the
+//    reference's right-first DFS meets first, so the winner is the reference's.
+//  any_hit: shadow rays stop at the first accepted triangle (only hitIdx == -1
+//    matters, :279).
+// ---------------------------------------------------------------------------
+struct Trav {
+    V3 o, d, inv;
+    int node, sp, hpos, fid;
+    float t, u, v;
+    bool any_hit;
+};
+
+__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
+    r.o = o;
+    r.d = d;
+    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
+    r.node = 0;
+    r.sp = 0;
+    r.hpos = -1;
+    r.fid = -1;
+    r.t = kRealMax;
+    r.u = 0.0f;
+    r.v = 0.0f;
+    r.any_hit = any_hit;
+}
+
+// Returns false once the traversal has finished (or overflowed its stack).
+// The stack region holds stack_depth + 1 slots so the push below may write
+// unconditionally (a write at sp == stack_depth lands in the spare slot).
+template <bool ORDERED, typename StackT>
+__device__ __forceinline__ bool trav_step(Trav& r, const float4* __restrict__ inner, const float4* __restrict__ tri,
+                                          int nint, StackT* stk, int stack_depth, uint32_t& c_inner,
+                                          uint32_t& c_leaf, uint32_t& c_ovf) {
+    int next = -1;
+    bool push = false, stop = false;
+    int deferred = 0;
+    if (r.node < nint) {
+        ++c_inner;
+        const float4* nd = inner + 4 * r.node;
+        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        float l0, l1, r0, r1;
+        bool hl = box_hit(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
+        bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
+        const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
+        if (ORDERED) {
+            const float lim = r.t * 1.0001f;
+            hl = hl & !(l0 > lim) & !(l1 < 0.5f * kDelta);
+            hr = hr & !(r0 > lim) & !(r1 < 0.5f * kDelta);
         }
-        if (sp == 0) break;
-        node = stk[(--sp) * 256];
+        const bool lfirst = ORDERED && (l0 < r0);   // reference order: right child first
+        push = hl & hr;
+        deferred = lfirst ? rc : lc;
+        next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
+    } else {
+        ++c_leaf;   // rayHitTriangle (geometry_queries.h:65-86), e1/e2 pre-gathered
+        const int pos = r.node - nint;
+        const float4* tr = tri + 3 * pos;
+        const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
+        const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
+        const V3 tv = r.o - v0;
+        const V3 p = cross(r.d, e2);
+        const V3 q = cross(tv, e1);
+        const float denom = dot(p, e1);
+        const float id = 1.0f / denom;
+        const float u = dot(p, tv) * id;
+        const float v = dot(q, r.d) * id;
+        const float t = dot(q, e2) * id;
+        const bool inside = (denom != 0.0f) & !((u < 0.0f) | (v < 0.0f) | (u + v > 1.0f));
+        const bool better = ORDERED ? ((t < r.t) | ((t == r.t) & (r.hpos >= 0) & (pos > r.hpos))) : (t < r.t);
+        const bool take = inside & better & (t > kDelta);   // :83
+        r.t = take ? t : r.t;
+        r.fid = take ? __float_as_int(q0.w) : r.fid;
+        r.u = take ? u : r.u;
+        r.v = take ? v : r.v;
+        r.hpos = take ? pos : r.hpos;
+        stop = take & r.any_hit;
     }
-    return h;
+    if (push) {
+        stk[r.sp * 256] = (StackT)deferred;
+        if (r.sp >= stack_depth) { ++c_ovf; return false; }
+        ++r.sp;
+    }
+    if (stop) return false;
+    if (next >= 0) {
+        r.node = next;
+        return true;
+    }
+    if (r.sp == 0) return false;
+    r.node = (int)stk[(--r.sp) * 256];
+    return true;
 }
 
 __device__ __forceinline__ V3 reflect_dir(V3 d, V3 n) { return d - (2.0f * dot(d, n)) * n; }   // :137-141
@@ -183,7 +213,7 @@ __device__ __forceinline__ float new_direction(V3 d, V3 n, float eta_m, float me
     const float cos_t = fsqrt(xorwow_uniform(st));
     const float sin_t = fsqrt(1.0f - cos_t * cos_t);
     float sp, cp;
-    psincos2pi(phi, sp, cp);
+    fsincos_2pi(phi, sp, cp);
     const float x = cp * sin_t;
     const float z = sp * sin_t;
     next = ((x * xb) + (cos_t * n)) + (z * zb);
@@ -245,267 +275,38 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
 }
 
 enum : int { PH_CAMERA = 0, PH_EXT = 1, PH_SHADOW = 2, PH_PROBE = 3 };
-
-// Per-lane path records, one per depth (path_tracer.cu:315-318): attenuation
-// (baseColor * atten), 1/p and the direct term, consumed by the unwind.
-template <int MAXD>
-struct PathRecords {
-    V3 att[MAXD], dst[MAXD];
-    float ivp[MAXD];
-};
-
-#ifndef TPT_TRACE_WAVES
-#define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator (96 VGPRs)
-#endif
-
-template <int MAXD, bool ORDERED>
-__global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
-    extern __shared__ int lds_stack[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
-    const bool active = x < a.width && ly < a.band_height && y < a.height;
-    uint32_t c_trav = 0, c_inner = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
-
-    if (active) {
-        const size_t npix = (size_t)a.width * (size_t)a.height;
-        const size_t off = (size_t)x + (size_t)y * (size_t)a.width;
-        const int nint = a.n_faces - 1;
-        int* stk = lds_stack + tid;
-        uint32_t st[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) st[i] = a.rng[i * npix + off];
-        V3 total = v3(a.accum[off], a.accum[npix + off], a.accum[2 * npix + off]);
-        PathRecords<MAXD> rec;
-
-        int remaining = a.samples;
-        int phase = PH_CAMERA;
-        int depth = 0, li = 0, mtl = 0;
-        V3 ro = v3(0.0f, 0.0f, 0.0f), rd = ro, td = ro, nd = ro, nrm = ro, direct = ro;
-
-        for (;;) {
-            if (phase == PH_CAMERA) {
-                if (remaining == 0) break;
-                --remaining;
-                // sampleRays (path_tracer.cu:42-59)
-                const float ju = xorwow_uniform(st);
-                const float jv = xorwow_uniform(st);
-                float lx = ju * 1.0f, lyf = jv * 1.0f;
-                lx = lx + (float)x;
-                lyf = lyf + (float)y;
-                lx = lx * a.inv_w;
-                lyf = lyf * a.inv_h;
-                lx = lx * a.sensor_w;
-                lyf = lyf * a.sensor_h;
-                float r4[4];
-                mat4_vec4(a.c2w, lx - a.half_sw, lyf - a.half_sh, 0.0f - 1.0f, 0.0f, r4);
-                rd = normalize(v3(r4[0], r4[1], r4[2]));
-                ro = v3(a.origin[0], a.origin[1], a.origin[2]);
-                td = rd;
-                depth = 0;
-                phase = PH_EXT;
-            }
-
-            ++c_trav;
-            const Hit h = traverse<ORDERED>(a.inner, a.tri, nint, stk, a.stack_depth, ro, td, phase == PH_SHADOW,
-                                            c_inner, c_leaf, c_ovf);
-
-            bool finish = false, lights_next = false, after = false;
-            V3 L = v3(0.0f, 0.0f, 0.0f);
-            if (phase == PH_EXT) {
-                if (h.fid < 0) {
-                    if (a.env) L = env_lookup(a.env, a.env_w, a.env_h, rd);
-                    finish = true;
-                } else {
-                    ++c_shade;
-                    const float4* sh = a.shade + 3 * h.fid;
-                    const float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
-                    const float w = 1.0f - h.u - h.v;
-                    nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (h.u * v3(s1.x, s1.y, s1.z))) +
-                                    (h.v * v3(s2.x, s2.y, s2.z)));
-                    ro = ro + (h.t * rd);
-                    mtl = __float_as_int(s0.w);
-                    const float4 m0 = a.mtl[2 * mtl], m1 = a.mtl[2 * mtl + 1];
-                    float af;
-                    const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
-                    rec.att[depth] = af * v3(m0.x, m0.y, m0.z);
-                    rec.ivp[depth] = 1.0f / prob;
-                    direct = v3(0.0f, 0.0f, 0.0f);
-                    li = 0;
-                    lights_next = true;
-                }
-            } else if (phase == PH_SHADOW) {
-                if (h.fid < 0) {   // sampleDeltaLights :279-282 (light re-sampled: deterministic)
-                    V3 ldir, lrad;
-                    light_sample(a.lights, li, ro, ldir, lrad);
-                    const float4 m0 = a.mtl[2 * mtl];
-                    direct = direct + (v3(m0.x, m0.y, m0.z) * lrad);
-                }
-                ++li;
-                lights_next = true;
-            } else {   // PH_PROBE (:390-400)
-                V3 dl = direct;
-                if (h.fid >= 0) {
-                    const int pm = __float_as_int(a.shade[3 * h.fid].w);
-                    const float e = a.mtl[2 * pm].w;
-                    dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + direct;
-                }
-                rec.dst[depth] = dl;
-                after = true;
-            }
-
-            if (lights_next) {
-                const float4 m1 = a.mtl[2 * mtl + 1];
-                if (li < a.n_lights) {
-                    V3 lrad;
-                    light_sample(a.lights, li, ro, td, lrad);
-                    phase = PH_SHADOW;
-                } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
-                    float af2;
-                    new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
-                    phase = PH_PROBE;
-                } else {
-                    rec.dst[depth] = direct;
-                    after = true;
-                }
-            }
-            if (after) {
-                const float e = a.mtl[2 * mtl].w;
-                if (e > 0.0f) {   // an emitter ends the path (:408-412); the unwind starts from e
-                    L = e * v3(1.0f, 1.0f, 1.0f);
-                    finish = true;
-                } else {
-                    rd = nd;
-                    td = rd;
-                    ++depth;
-                    if (depth == a.max_depth) finish = true;
-                    else phase = PH_EXT;
-                }
-            }
-            if (finish) {   // unwind (:416-431): levels depth-1 .. 0
-                for (int k = depth - 1; k >= 0; --k) L = rec.ivp[k] * ((rec.dst[k] + L) * rec.att[k]);
-                total = total + L;
-                phase = PH_CAMERA;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 6; ++i) a.rng[i * npix + off] = st[i];
-        a.accum[off] = total.x;
-        a.accum[npix + off] = total.y;
-        a.accum[2 * npix + off] = total.z;
-    }
-
-    const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
-                             s_shade = wave_sum(c_shade), s_ovf = wave_sum(c_ovf);
-    if (lane == 0) {
-        atomicAdd(&a.counters[0], s_trav);
-        atomicAdd(&a.counters[1], s_inner);
-        atomicAdd(&a.counters[2], s_leaf);
-        atomicAdd(&a.counters[3], s_shade);
-        if (s_ovf) atomicAdd(&a.counters[4], s_ovf);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// v3 megakernel: ballot-driven traversal with postponed shading.
-//
-// A wave keeps stepping its lanes through BVH nodes while at least
-// `a.refill` of them are still traversing; once fewer are, it leaves the loop
-// and the finished lanes shade their hit, advance their path state machine and
-// set up their next ray (next bounce, shadow, probe or next sample), while the
-// unfinished lanes keep their traversal state (node, stack, best hit) in
-// registers and resume afterwards.  The wave therefore pays for the average
-// traversal length of its lanes instead of the longest one.
-// ---------------------------------------------------------------------------
-struct Trav {
-    V3 o, d, inv;
-    int node, sp, hpos, fid;
-    float t, u, v;
-    bool any_hit;
-};
-
-__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
-    r.o = o;
-    r.d = d;
-    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    r.node = 0;
-    r.sp = 0;
-    r.hpos = -1;
-    r.fid = -1;
-    r.t = kRealMax;
-    r.u = 0.0f;
-    r.v = 0.0f;
-    r.any_hit = any_hit;
-}
-
-// One node of traverseBVH (path_tracer.cu:61-107), same semantics as
-// traverse<ORDERED> above.  Returns false once the traversal has finished.
-template <bool ORDERED>
-__device__ __forceinline__ bool trav_step(Trav& r, const float4* __restrict__ inner, const float4* __restrict__ tri,
-                                          int nint, int* stk, int stack_depth, uint32_t& c_inner, uint32_t& c_leaf,
-                                          uint32_t& c_ovf) {
-    if (r.node < nint) {
-        ++c_inner;
-        const float4* nd = inner + 4 * r.node;
-        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        float l0, l1, r0, r1;
-        bool hl = box_hit(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
-        bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
-        const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
-        if (ORDERED) {
-            const float lim = r.t * 1.0001f;
-            hl = hl && !(l0 > lim) && !(l1 < 0.5f * kDelta);
-            hr = hr && !(r0 > lim) && !(r1 < 0.5f * kDelta);
-        }
-        if (hl && hr) {
-            int first = rc, second = lc;
-            if (ORDERED && l0 < r0) { first = lc; second = rc; }
-            if (r.sp >= stack_depth) { ++c_ovf; return false; }
-            stk[(r.sp++) * 256] = second;
-            r.node = first;
-            return true;
-        }
-        if (hl) { r.node = lc; return true; }
-        if (hr) { r.node = rc; return true; }
-    } else {
-        ++c_leaf;
-        const int pos = r.node - nint;
-        const float4* tr = tri + 3 * pos;
-        const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
-        const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
-        const V3 tv = r.o - v0;
-        const V3 p = cross(r.d, e2);
-        const V3 q = cross(tv, e1);
-        const float denom = dot(p, e1);
-        if (denom != 0.0f) {
-            const float id = 1.0f / denom;
-            const float u = dot(p, tv) * id;
-            const float v = dot(q, r.d) * id;
-            if (!(u < 0.0f || v < 0.0f || u + v > 1.0f)) {
-                const float t = dot(q, e2) * id;
-                const bool better = ORDERED ? (t < r.t || (t == r.t && r.hpos >= 0 && pos > r.hpos)) : (t < r.t);
-                if (better && t > kDelta) {
-                    r.t = t;
-                    r.fid = __float_as_int(q0.w);
-                    r.u = u;
-                    r.v = v;
-                    r.hpos = pos;
-                    if (r.any_hit) return false;
-                }
-            }
-        }
-    }
-    if (r.sp == 0) return false;
-    r.node = stk[(--r.sp) * 256];
-    return true;
-}
-
 enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2 };
 
-template <int MAXD, bool ORDERED>
-__global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
-    extern __shared__ int lds_stack[];
+// Per-lane path records (path_tracer.cu:315-318): attenuation = baseColor *
+// atten (3), 1/p (1) and the direct term (3) per depth, consumed by the unwind
+// (:416-430).  Levels < kLdsLevels live in LDS ([word][lane]), deeper ones in
+// private memory.
+constexpr int kLdsLevels = 2;
+constexpr int kRecWords = 7;
+
+template <int MAXD>
+struct PathRecords {
+    float* lds;                          // this lane's column: word w at lds[w * 256]
+    float deep[MAXD > kLdsLevels ? (MAXD - kLdsLevels) * kRecWords : 1];
+
+    __device__ __forceinline__ void put(int level, int w, float v) {
+        if (level < kLdsLevels) lds[(level * kRecWords + w) * 256] = v;
+        else deep[(level - kLdsLevels) * kRecWords + w] = v;
+    }
+    __device__ __forceinline__ float get(int level, int w) const {
+        return level < kLdsLevels ? lds[(level * kRecWords + w) * 256] : deep[(level - kLdsLevels) * kRecWords + w];
+    }
+    __device__ __forceinline__ void put_att(int level, V3 att, float ivp) {
+        put(level, 0, att.x); put(level, 1, att.y); put(level, 2, att.z); put(level, 3, ivp);
+    }
+    __device__ __forceinline__ void put_dst(int level, V3 dst) {
+        put(level, 4, dst.x); put(level, 5, dst.y); put(level, 6, dst.z);
+    }
+};
+
+template <int MAXD, bool ORDERED, typename StackT>
+__global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
@@ -515,7 +316,9 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
     const int nint = a.n_faces - 1;
-    int* stk = lds_stack + tid;
+    StackT* stk = (StackT*)lds + tid;
+    PathRecords<MAXD> rec;
+    rec.lds = (float*)(lds + a.lds_rec_offset) + tid;
 
     uint32_t st[6];
     V3 total = v3(0.0f, 0.0f, 0.0f);
@@ -524,7 +327,6 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
         for (int i = 0; i < 6; ++i) st[i] = a.rng[i * npix + off];
         total = v3(a.accum[off], a.accum[npix + off], a.accum[2 * npix + off]);
     }
-    PathRecords<MAXD> rec;
     int remaining = a.samples;
     int phase = PH_CAMERA;
     int depth = 0, li = 0, mtl = 0;
@@ -536,14 +338,14 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
 
     for (;;) {
         if (ts == TS_DONE) {
-            // ---- consume the finished traversal (none for a fresh sample) ----
+            // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
             V3 L = v3(0.0f, 0.0f, 0.0f);
             if (phase == PH_EXT) {
-                if (r.fid < 0) {
+                if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
                     if (a.env) L = env_lookup(a.env, a.env_w, a.env_h, rd);
                     finish = true;
-                } else {
+                } else {           // hit shading prelude (:364-381)
                     ++c_shade;
                     const float4* sh = a.shade + 3 * r.fid;
                     const float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
@@ -555,8 +357,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
                     const float4 m0 = a.mtl[2 * mtl], m1 = a.mtl[2 * mtl + 1];
                     float af;
                     const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
-                    rec.att[depth] = af * v3(m0.x, m0.y, m0.z);
-                    rec.ivp[depth] = 1.0f / prob;
+                    rec.put_att(depth, af * v3(m0.x, m0.y, m0.z), 1.0f / prob);
                     direct = v3(0.0f, 0.0f, 0.0f);
                     li = 0;
                     lights_next = true;
@@ -577,7 +378,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
                     const float e = a.mtl[2 * pm].w;
                     dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + direct;
                 }
-                rec.dst[depth] = dl;
+                rec.put_dst(depth, dl);
                 after = true;
             }
             V3 td = rd;
@@ -594,7 +395,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
                     new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
                     phase = PH_PROBE;
                 } else {
-                    rec.dst[depth] = direct;
+                    rec.put_dst(depth, direct);
                     after = true;
                 }
             }
@@ -612,7 +413,11 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
                 }
             }
             if (finish) {   // unwind (:416-431): levels depth-1 .. 0
-                for (int k = depth - 1; k >= 0; --k) L = rec.ivp[k] * ((rec.dst[k] + L) * rec.att[k]);
+                for (int k = depth - 1; k >= 0; --k) {
+                    const V3 att = v3(rec.get(k, 0), rec.get(k, 1), rec.get(k, 2));
+                    const V3 dst = v3(rec.get(k, 4), rec.get(k, 5), rec.get(k, 6));
+                    L = rec.get(k, 3) * ((dst + L) * att);
+                }
                 total = total + L;
                 phase = PH_CAMERA;
             }
@@ -650,8 +455,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace3(TraceArgs a) {
         if (__ballot(ts != TS_DEAD) == 0ull) break;
         // ---- traversal: step while enough lanes of the wave are still traversing ----
         for (;;) {
-            const unsigned long long tm = __ballot(ts == TS_TRAV);
-            const int cnt = __popcll(tm);
+            const int cnt = __popcll(__ballot(ts == TS_TRAV));
             if (cnt == 0) break;
             if (cnt < refill && __ballot(ts == TS_DONE) != 0ull) break;
             if (ts == TS_TRAV) {
@@ -704,55 +508,55 @@ __global__ void k_resolve(ResolveArgs a) {
     }
 }
 
+// Closest hit for a batch of rays in the reference's visit order (tests).
 __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, const float* __restrict__ o,
                                                     const float* __restrict__ d, int32_t* hit, float* t, float* uv) {
-    extern __shared__ int lds_stack[];
+    extern __shared__ __attribute__((aligned(16))) char lds[];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     uint32_t c0 = 0, c1 = 0, c2 = 0;
     if (i < n) {
-        const Hit h = traverse<false>(a.inner, a.tri, a.n_faces - 1, lds_stack + threadIdx.x, a.stack_depth,
-                               v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
-                               false, c0, c1, c2);
-        hit[i] = h.fid;
-        t[i] = h.t;
-        uv[2 * i] = h.u;
-        uv[2 * i + 1] = h.v;
+        Trav r;
+        trav_begin(r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]), false);
+        while (trav_step<false>(r, a.inner, a.tri, a.n_faces - 1, (int*)lds + threadIdx.x, a.stack_depth, c0, c1,
+                                c2)) {
+        }
+        hit[i] = r.fid;
+        t[i] = r.t;
+        uv[2 * i] = r.u;
+        uv[2 * i + 1] = r.v;
     }
 }
 
-template <bool ORDERED, bool V3K>
+template <bool ORDERED, typename StackT>
 static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if (V3K) {
-        if (a.max_depth <= 8)
-            hipLaunchKernelGGL((k_trace3<8, ORDERED>), grid, dim3(256), lds, s, a);
-        else if (a.max_depth <= 16)
-            hipLaunchKernelGGL((k_trace3<16, ORDERED>), grid, dim3(256), lds, s, a);
-        else if (a.max_depth <= 32)
-            hipLaunchKernelGGL((k_trace3<32, ORDERED>), grid, dim3(256), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_trace3<64, ORDERED>), grid, dim3(256), lds, s, a);
-        return;
-    }
     if (a.max_depth <= 8)
-        hipLaunchKernelGGL((k_trace<8, ORDERED>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_trace<8, ORDERED, StackT>), grid, dim3(256), lds, s, a);
     else if (a.max_depth <= 16)
-        hipLaunchKernelGGL((k_trace<16, ORDERED>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_trace<16, ORDERED, StackT>), grid, dim3(256), lds, s, a);
     else if (a.max_depth <= 32)
-        hipLaunchKernelGGL((k_trace<32, ORDERED>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_trace<32, ORDERED, StackT>), grid, dim3(256), lds, s, a);
     else
-        hipLaunchKernelGGL((k_trace<64, ORDERED>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_trace<64, ORDERED, StackT>), grid, dim3(256), lds, s, a);
 }
 
-hipError_t launch_trace(const TraceArgs& a, hipStream_t s) {
+size_t trace_lds_bytes(const TraceArgs& a, int* rec_offset) {
+    const size_t elem = (2 * (size_t)a.n_faces - 1) <= 65535 ? 2 : 4;
+    const size_t stack = ((size_t)(a.stack_depth + 1) * 256 * elem + 15) / 16 * 16;
+    *rec_offset = (int)stack;
+    return stack + (size_t)kLdsLevels * kRecWords * 256 * sizeof(float);
+}
+
+hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
+    TraceArgs a = a_in;
+    const size_t lds = trace_lds_bytes(a, &a.lds_rec_offset);
     dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
-    const size_t lds = (size_t)a.stack_depth * 256 * sizeof(int);
-    const bool legacy = (a.flags & TPT_FLAG_LEGACY_LOOP) != 0;
+    const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
     if (a.flags & TPT_FLAG_REF_ORDER) {
-        if (legacy) launch_trace_t<false, false>(a, grid, lds, s);
-        else launch_trace_t<false, true>(a, grid, lds, s);
+        if (small) launch_trace_t<false, uint16_t>(a, grid, lds, s);
+        else launch_trace_t<false, int>(a, grid, lds, s);
     } else {
-        if (legacy) launch_trace_t<true, false>(a, grid, lds, s);
-        else launch_trace_t<true, true>(a, grid, lds, s);
+        if (small) launch_trace_t<true, uint16_t>(a, grid, lds, s);
+        else launch_trace_t<true, int>(a, grid, lds, s);
     }
     return hipGetLastError();
 }
@@ -766,7 +570,7 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
 hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int32_t* hit, float* t,
                              float* uv, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const size_t lds = (size_t)a.stack_depth * 256 * sizeof(int);
+    const size_t lds = (size_t)(a.stack_depth + 1) * 256 * sizeof(int);
     hipLaunchKernelGGL(k_trace_rays, dim3((n + 255) / 256), dim3(256), lds, s, a, n, o, d, hit, t, uv);
     return hipGetLastError();
 }
