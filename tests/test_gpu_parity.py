@@ -13,7 +13,9 @@ import pytest
 
 import tinypathtracer_amd as T
 from oracle import oracle as O
-from tests.conftest import scene_path
+import os
+
+from tests.conftest import ROOT, scene_path
 
 pytestmark = pytest.mark.gpu
 
@@ -243,3 +245,25 @@ def test_pathtracer_render_api():
     fr = pt.render(scene_path("box"), nSamplesPerPixel=4, seed=1)
     assert fr.bgra.shape == (18, 32, 4) and fr.radiance.shape == (18, 32, 3)
     assert fr.stats["traversals"] > 0 and fr.radiance.mean() > 0.01
+
+
+def test_cpp_cli_matches_python_host(tmp_path):
+    """tpt_render (C++ host API, include/tpt.hpp) renders the same frame as the
+    Python host mirror through the same C-ABI."""
+    import subprocess
+    exe = os.path.join(ROOT, "tinypathtracer_amd", "tpt_render")
+    W, H, spp = 48, 27, 8
+    out = str(tmp_path / "cli")
+    res = subprocess.run([exe, scene_path("box"), "--width", str(W), "--height", str(H), "--spp", str(spp),
+                          "--seed", "42", "--out", out], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    with open(out + ".pfm", "rb") as f:
+        for _ in range(3):
+            f.readline()
+        pfm = np.frombuffer(f.read(), np.float32).reshape(H, W, 3)
+    s = T.Scene(scene_path("box"))
+    d = s.copySceneToDevice(0).build()
+    rad = np.zeros((H, W, 3), np.float32)
+    T.PathTracer("", W, H, 0).doTrace(d, s.m_camera, None, spp, seed=42, radiance=rad)
+    d.close()
+    assert np.array_equal(pfm.view(np.uint32), rad.view(np.uint32))
