@@ -57,7 +57,8 @@ struct TraceArgs {
     int32_t samples;                     // samples for this launch
     int32_t flags;
     int32_t refill;                      // leave the traversal loop below this many active lanes
-    int32_t lds_rec_offset;              // set by launch_trace
+    int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
+    int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
     // per-pixel state (SoA over W*H pixels)
     uint32_t* rng;                       // 6 planes: v0..v4, d
     float* accum;                        // 3 planes: r, g, b (running totalRad)

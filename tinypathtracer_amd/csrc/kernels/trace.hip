@@ -277,30 +277,39 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
 enum : int { PH_CAMERA = 0, PH_EXT = 1, PH_SHADOW = 2, PH_PROBE = 3 };
 enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2 };
 
-// Per-lane path records (path_tracer.cu:315-318): attenuation = baseColor *
-// atten (3), 1/p (1) and the direct term (3) per depth, consumed by the unwind
-// (:416-430).  Levels < kLdsLevels live in LDS ([word][lane]), deeper ones in
+// Per-lane path records (path_tracer.cu:315-318), consumed by the unwind
+// (:416-430).  The reference keeps attenuation = baseColor * atten (3 floats),
+// p and the direct term (3) per depth.  Stored here, bit-equivalently:
+//   w0 atten, w1 p, w2 material id  -> attenuation = atten * base and 1/p are
+//                                      recomputed at unwind (same operations)
+//   w3..w5 direct term; with no delta lights the direct term is (e, e, e) --
+//   all three channels come from the same emission scalar -- so one word.
+// Levels < a.rec_lds_levels live in LDS ([level][word][lane]); deeper ones in
 // private memory.
-constexpr int kLdsLevels = 2;
-constexpr int kRecWords = 7;
-
 template <int MAXD>
 struct PathRecords {
-    float* lds;                          // this lane's column: word w at lds[w * 256]
-    float deep[MAXD > kLdsLevels ? (MAXD - kLdsLevels) * kRecWords : 1];
+    float* lds;                          // this lane's column: word at lds[(level*words + w) * 256]
+    int nlds, words;
+    float deep[MAXD * 6];
 
     __device__ __forceinline__ void put(int level, int w, float v) {
-        if (level < kLdsLevels) lds[(level * kRecWords + w) * 256] = v;
-        else deep[(level - kLdsLevels) * kRecWords + w] = v;
+        if (level < nlds) lds[(level * words + w) * 256] = v;
+        else deep[level * 6 + w] = v;
     }
     __device__ __forceinline__ float get(int level, int w) const {
-        return level < kLdsLevels ? lds[(level * kRecWords + w) * 256] : deep[(level - kLdsLevels) * kRecWords + w];
+        return level < nlds ? lds[(level * words + w) * 256] : deep[level * 6 + w];
     }
-    __device__ __forceinline__ void put_att(int level, V3 att, float ivp) {
-        put(level, 0, att.x); put(level, 1, att.y); put(level, 2, att.z); put(level, 3, ivp);
+    __device__ __forceinline__ void put_shade(int level, float atten, float prob, int mtl) {
+        put(level, 0, atten);
+        put(level, 1, prob);
+        put(level, 2, __int_as_float(mtl));
     }
     __device__ __forceinline__ void put_dst(int level, V3 dst) {
-        put(level, 4, dst.x); put(level, 5, dst.y); put(level, 6, dst.z);
+        put(level, 3, dst.x);
+        if (words > 4) {
+            put(level, 4, dst.y);
+            put(level, 5, dst.z);
+        }
     }
 };
 
@@ -319,6 +328,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     StackT* stk = (StackT*)lds + tid;
     PathRecords<MAXD> rec;
     rec.lds = (float*)(lds + a.lds_rec_offset) + tid;
+    rec.nlds = a.rec_lds_levels;
+    rec.words = a.n_lights > 0 ? 6 : 4;
 
     uint32_t st[6];
     V3 total = v3(0.0f, 0.0f, 0.0f);
@@ -357,7 +368,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     const float4 m0 = a.mtl[2 * mtl], m1 = a.mtl[2 * mtl + 1];
                     float af;
                     const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
-                    rec.put_att(depth, af * v3(m0.x, m0.y, m0.z), 1.0f / prob);
+                    (void)m0;
+                    rec.put_shade(depth, af, prob, mtl);
                     direct = v3(0.0f, 0.0f, 0.0f);
                     li = 0;
                     lights_next = true;
@@ -414,9 +426,12 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             }
             if (finish) {   // unwind (:416-431): levels depth-1 .. 0
                 for (int k = depth - 1; k >= 0; --k) {
-                    const V3 att = v3(rec.get(k, 0), rec.get(k, 1), rec.get(k, 2));
-                    const V3 dst = v3(rec.get(k, 4), rec.get(k, 5), rec.get(k, 6));
-                    L = rec.get(k, 3) * ((dst + L) * att);
+                    const float4 mb = a.mtl[2 * __float_as_int(rec.get(k, 2))];
+                    const V3 att = rec.get(k, 0) * v3(mb.x, mb.y, mb.z);       // :379
+                    const float ivp = 1.0f / rec.get(k, 1);                     // :427 "/ pStack"
+                    const float d0 = rec.get(k, 3);
+                    const V3 dst = rec.words > 4 ? v3(d0, rec.get(k, 4), rec.get(k, 5)) : v3(d0, d0, d0);
+                    L = ivp * ((dst + L) * att);
                 }
                 total = total + L;
                 phase = PH_CAMERA;
@@ -539,16 +554,24 @@ static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_
         hipLaunchKernelGGL((k_trace<64, ORDERED, StackT>), grid, dim3(256), lds, s, a);
 }
 
-size_t trace_lds_bytes(const TraceArgs& a, int* rec_offset) {
+// LDS per 256-lane workgroup: the traversal stack, then as many path-record
+// levels as fit in kLdsBudget (5 workgroups per CU share the 160 KiB).
+constexpr size_t kLdsBudget = 32768;
+
+size_t trace_lds_bytes(TraceArgs& a) {
     const size_t elem = (2 * (size_t)a.n_faces - 1) <= 65535 ? 2 : 4;
     const size_t stack = ((size_t)(a.stack_depth + 1) * 256 * elem + 15) / 16 * 16;
-    *rec_offset = (int)stack;
-    return stack + (size_t)kLdsLevels * kRecWords * 256 * sizeof(float);
+    const size_t level = (a.n_lights > 0 ? 6 : 4) * 256 * sizeof(float);
+    size_t levels = stack < kLdsBudget ? (kLdsBudget - stack) / level : 0;
+    if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;
+    a.lds_rec_offset = (int)stack;
+    a.rec_lds_levels = (int)levels;
+    return stack + levels * level;
 }
 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
-    const size_t lds = trace_lds_bytes(a, &a.lds_rec_offset);
+    const size_t lds = trace_lds_bytes(a);
     dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
     const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
     if (a.flags & TPT_FLAG_REF_ORDER) {

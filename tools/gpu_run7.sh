@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -x -p no:cacheprovider > gpurun_out/pytest_gpu8.log 2>&1; echo PYTEST=$?
-tail -3 gpurun_out/pytest_gpu8.log
-bash tools/sweep_variants.sh > gpurun_out/sweep5.log 2>&1; cat gpurun_out/sweep5.log
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu9.log 2>&1; echo PYTEST=$?
+tail -3 gpurun_out/pytest_gpu9.log
+bash tools/sweep_variants.sh > gpurun_out/sweep7.log 2>&1; cat gpurun_out/sweep7.log
