@@ -57,6 +57,7 @@ struct TraceArgs {
     int32_t samples;                     // samples for this launch
     int32_t flags;
     int32_t refill;                      // leave the traversal loop below this many active lanes
+    int32_t boxes_finite;                // all node boxes finite: min/max slab test is exact
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
     // per-pixel state (SoA over W*H pixels)
@@ -64,6 +65,13 @@ struct TraceArgs {
     float* accum;                        // 3 planes: r, g, b (running totalRad)
     unsigned long long* counters;        // [0] trav [1] inner [2] leaf [3] shade [4] overflow
 };
+
+// Path-record words per bounce (k_trace): 2 when the scene has no delta lights
+// (atten; material | probe material | p-kind packed), else 5 (atten; material |
+// p-kind; direct term x3).  The packed form needs material ids below 0x7fff.
+__host__ __device__ inline int rec_words(int n_lights, int n_materials) {
+    return (n_lights > 0 || n_materials >= 0x7ffe) ? 5 : 2;
+}
 
 struct ResolveArgs {
     const float* accum;
@@ -103,7 +111,7 @@ struct BuildBuffers {
     uint32_t* parent;                    // 2F-1
     float* node_box;                     // 6 per node (2F-1)
     uint32_t* flags;                     // F-1
-    uint32_t* max_depth;                 // 1
+    uint32_t* max_depth;                 // 2: deepest leaf, non-finite inner-box flag
     void* sort_tmp;
     size_t sort_tmp_bytes;
     // outputs
@@ -112,6 +120,7 @@ struct BuildBuffers {
     float4* shade;
     void* nodes36;                       // reference layout (2F-1) * 36 B
     uint32_t out_max_depth;              // deepest leaf (root = 0), set by launch_build
+    uint32_t out_boxes_finite;           // 1: every inner-node child box is finite
 };
 hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes);
 hipError_t launch_build(BuildBuffers& b, hipStream_t s);

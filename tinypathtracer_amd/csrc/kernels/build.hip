@@ -192,6 +192,10 @@ __global__ void k_pack_inner(BuildBuffers b) {
     q[1] = make_float4(l[4], l[5], r[0], r[1]);
     q[2] = make_float4(r[2], r[3], r[4], r[5]);
     q[3] = make_float4(__int_as_float(c.x), __int_as_float(c.y), 0.0f, 0.0f);
+    bool fin = true;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) fin = fin && isfinite(l[k]) && isfinite(r[k]);
+    if (!fin) atomicOr(b.max_depth + 1, 1u);
 }
 
 __global__ void k_pack_leaf(BuildBuffers b) {
@@ -273,7 +277,7 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s) {
         TPT_TRY(hipGetLastError());
     }
     uint32_t* depth = b.flags;   // reused: 2F-1 words
-    TPT_TRY(hipMemsetAsync(b.max_depth, 0, sizeof(uint32_t), s));
+    TPT_TRY(hipMemsetAsync(b.max_depth, 0, 2 * sizeof(uint32_t), s));
     hipLaunchKernelGGL(k_depth, grid(nn), blk, 0, s, b, depth);
     TPT_TRY(hipGetLastError());
     uint32_t maxd = 0;
@@ -295,7 +299,11 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s) {
     TPT_TRY(hipGetLastError());
     hipLaunchKernelGGL(k_pack_nodes36, grid(nn), blk, 0, s, b);
     TPT_TRY(hipGetLastError());
-    return hipStreamSynchronize(s);
+    uint32_t nonfinite = 0;
+    TPT_TRY(hipMemcpyAsync(&nonfinite, b.max_depth + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    TPT_TRY(hipStreamSynchronize(s));
+    b.out_boxes_finite = nonfinite ? 0u : 1u;
+    return hipSuccess;
 }
 
 }  // namespace tpt

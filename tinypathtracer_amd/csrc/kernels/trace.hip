@@ -26,6 +26,15 @@
 #include "../common/tpt_math.hpp"
 #include "tpt.h"
 
+#ifndef TPT_LEAF_SPEC
+#define TPT_LEAF_SPEC 1   // speculative leaf postponement (k_trace)
+#endif
+#ifndef TPT_LEAF_KB
+#define TPT_LEAF_KB 8     // run the triangle branch once this many lanes are blocked ...
+#endif
+#ifndef TPT_LEAF_KP
+#define TPT_LEAF_KP 24    // ... or this many lanes hold a parked leaf
+#endif
 #ifndef TPT_TRACE_WAVES
 #define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator
 #endif
@@ -84,8 +93,10 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 struct Trav {
     V3 o, d, inv;
     int node, sp, hpos, fid;
+    int pend;   // parked leaf position (speculative traversal), -1: none
     float t, u, v;
     bool any_hit;
+    bool fin;   // origin and 1/dir finite: no slab product can be NaN
 };
 
 __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
@@ -94,12 +105,98 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
     r.node = 0;
     r.sp = 0;
+    r.pend = -1;
     r.hpos = -1;
     r.fid = -1;
     r.t = kRealMax;
     r.u = 0.0f;
     r.v = 0.0f;
     r.any_hit = any_hit;
+    r.fin = __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
+            __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
+}
+
+// Visit of inner node r.node: the child to descend into (-1: none) and, when
+// both children are entered, the deferred one to push.
+template <bool ORDERED>
+__device__ __forceinline__ void inner_visit(const Trav& r, const float4* __restrict__ inner, int& next, bool& push,
+                                            int& deferred) {
+    const float4* nd = inner + 4 * r.node;
+    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+    float l0, l1, r0, r1;
+    bool hl = box_hit(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
+    bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
+    const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
+    if (ORDERED) {
+        const float lim = r.t * 1.0001f;
+        hl = hl & !(l0 > lim) & !(l1 < 0.5f * kDelta);
+        hr = hr & !(r0 > lim) & !(r1 < 0.5f * kDelta);
+    }
+    const bool lfirst = ORDERED && (l0 < r0);   // reference order: right child first
+    push = hl & hr;
+    deferred = lfirst ? rc : lc;
+    next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
+}
+
+// The same ordered visit through min/max slab arithmetic, for rays and boxes
+// whose slab products cannot be NaN (finite origin, 1/dir and box bounds).
+// Then lo <= hi on every axis and the reference's sequential test (miss as soon
+// as max(-R, lo..) > min(R, hi..) for the axes seen so far) reduces to
+// T0 = max(lo_x, lo_y, lo_z) <= T1 = min(R, hi_x, hi_y, hi_z) -- any crossed
+// pair (lo_i > hi_j) is caught at the later of the two axes -- and the two
+// culls fold in: hit & T0 <= lim & T1 >= Delta/2  <=>  max(T0, Delta/2) <=
+// min(T1, R, lim), since Delta/2 > -R and lim > Delta/2.  Signed zeros may
+// differ from the ternaries; only comparisons consume T0/T1.
+__device__ __forceinline__ void slab_minmax(const V3& o, const V3& inv, float nx, float ny, float nz, float xx,
+                                            float xy, float xz, float& t0, float& t1) {
+    const float ax = (nx - o.x) * inv.x, bx = (xx - o.x) * inv.x;
+    const float ay = (ny - o.y) * inv.y, by = (xy - o.y) * inv.y;
+    const float az = (nz - o.z) * inv.z, bz = (xz - o.z) * inv.z;
+    t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+}
+
+__device__ __forceinline__ void inner_visit_fast(const Trav& r, const float4* __restrict__ inner, int& next,
+                                                 bool& push, int& deferred) {
+    const float4* nd = inner + 4 * r.node;
+    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+    float l0, l1, r0, r1;
+    slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
+    slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
+    const float hi = fminf(kRealMax, r.t * 1.0001f);
+    const bool hl = fmaxf(l0, 0.5f * kDelta) <= fminf(l1, hi);
+    const bool hr = fmaxf(r0, 0.5f * kDelta) <= fminf(r1, hi);
+    const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
+    const bool lfirst = l0 < r0;
+    push = hl & hr;
+    deferred = lfirst ? rc : lc;
+    next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
+}
+
+// rayHitTriangle (geometry_queries.h:65-86) on leaf position pos, e1/e2
+// pre-gathered.  Returns true when an any-hit ray may stop.
+template <bool ORDERED>
+__device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos) {
+    const float4* tr = tri + 3 * pos;
+    const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
+    const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
+    const V3 tv = r.o - v0;
+    const V3 p = cross(r.d, e2);
+    const V3 q = cross(tv, e1);
+    const float denom = dot(p, e1);
+    const float id = 1.0f / denom;
+    const float u = dot(p, tv) * id;
+    const float v = dot(q, r.d) * id;
+    const float t = dot(q, e2) * id;
+    const bool inside = (denom != 0.0f) & !((u < 0.0f) | (v < 0.0f) | (u + v > 1.0f));
+    const bool better = ORDERED ? ((t < r.t) | ((t == r.t) & (r.hpos >= 0) & (pos > r.hpos))) : (t < r.t);
+    const bool take = inside & better & (t > kDelta);   // :83
+    r.t = take ? t : r.t;
+    r.fid = take ? __float_as_int(q0.w) : r.fid;
+    r.u = take ? u : r.u;
+    r.v = take ? v : r.v;
+    r.hpos = take ? pos : r.hpos;
+    return take & r.any_hit;
 }
 
 // Returns false once the traversal has finished (or overflowed its stack).
@@ -114,44 +211,10 @@ __device__ __forceinline__ bool trav_step(Trav& r, const float4* __restrict__ in
     int deferred = 0;
     if (r.node < nint) {
         ++c_inner;
-        const float4* nd = inner + 4 * r.node;
-        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        float l0, l1, r0, r1;
-        bool hl = box_hit(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
-        bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
-        const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
-        if (ORDERED) {
-            const float lim = r.t * 1.0001f;
-            hl = hl & !(l0 > lim) & !(l1 < 0.5f * kDelta);
-            hr = hr & !(r0 > lim) & !(r1 < 0.5f * kDelta);
-        }
-        const bool lfirst = ORDERED && (l0 < r0);   // reference order: right child first
-        push = hl & hr;
-        deferred = lfirst ? rc : lc;
-        next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
+        inner_visit<ORDERED>(r, inner, next, push, deferred);
     } else {
-        ++c_leaf;   // rayHitTriangle (geometry_queries.h:65-86), e1/e2 pre-gathered
-        const int pos = r.node - nint;
-        const float4* tr = tri + 3 * pos;
-        const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
-        const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
-        const V3 tv = r.o - v0;
-        const V3 p = cross(r.d, e2);
-        const V3 q = cross(tv, e1);
-        const float denom = dot(p, e1);
-        const float id = 1.0f / denom;
-        const float u = dot(p, tv) * id;
-        const float v = dot(q, r.d) * id;
-        const float t = dot(q, e2) * id;
-        const bool inside = (denom != 0.0f) & !((u < 0.0f) | (v < 0.0f) | (u + v > 1.0f));
-        const bool better = ORDERED ? ((t < r.t) | ((t == r.t) & (r.hpos >= 0) & (pos > r.hpos))) : (t < r.t);
-        const bool take = inside & better & (t > kDelta);   // :83
-        r.t = take ? t : r.t;
-        r.fid = take ? __float_as_int(q0.w) : r.fid;
-        r.u = take ? u : r.u;
-        r.v = take ? v : r.v;
-        r.hpos = take ? pos : r.hpos;
-        stop = take & r.any_hit;
+        ++c_leaf;
+        stop = leaf_test<ORDERED>(r, tri, r.node - nint);
     }
     if (push) {
         stk[r.sp * 256] = (StackT)deferred;
@@ -280,35 +343,46 @@ enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2 };
 // Per-lane path records (path_tracer.cu:315-318), consumed by the unwind
 // (:416-430).  The reference keeps attenuation = baseColor * atten (3 floats),
 // p and the direct term (3) per depth.  Stored here, bit-equivalently:
-//   w0 atten, w1 p, w2 material id  -> attenuation = atten * base and 1/p are
-//                                      recomputed at unwind (same operations)
-//   w3..w5 direct term; with no delta lights the direct term is (e, e, e) --
-//   all three channels come from the same emission scalar -- so one word.
+//   w0 atten -- attenuation = atten * base is recomputed at unwind (same op);
+//   p is atten itself (dielectric and metal: 1 and 1; diffuse with c > 0:
+//     |c|/pi == (c/pi)*1) or a signed zero (c <= 0): a 2-bit kind in w1 bits
+//     30-31 (a NaN c keeps its NaN, only the NaN's sign may differ);
+//   w1 bits 0-14 material id;
+//   no delta lights (rec_words == 2): the direct term is exactly
+//     (1*e) + 0 of the material the probe ray hit, or 0 -- its id in w1 bits
+//     15-29 (0x7fff: none);
+//   delta lights (rec_words == 5): material id in bits 0-29, w2..w4 direct.
 // Levels < a.rec_lds_levels live in LDS ([level][word][lane]); deeper ones in
 // private memory.
+constexpr uint32_t kNoProbe = 0x7fffu;
+
+__device__ __forceinline__ uint32_t p_kind(float prob) {
+    const uint32_t pb = __float_as_uint(prob);
+    return pb == 0x80000000u ? 1u : (pb == 0u ? 2u : 0u);
+}
+
 template <int MAXD>
 struct PathRecords {
     float* lds;                          // this lane's column: word at lds[(level*words + w) * 256]
     int nlds, words;
-    float deep[MAXD * 6];
+    float deep[MAXD * 5];
 
     __device__ __forceinline__ void put(int level, int w, float v) {
         if (level < nlds) lds[(level * words + w) * 256] = v;
-        else deep[level * 6 + w] = v;
+        else deep[level * 5 + w] = v;
     }
     __device__ __forceinline__ float get(int level, int w) const {
-        return level < nlds ? lds[(level * words + w) * 256] : deep[level * 6 + w];
+        return level < nlds ? lds[(level * words + w) * 256] : deep[level * 5 + w];
     }
-    __device__ __forceinline__ void put_shade(int level, float atten, float prob, int mtl) {
-        put(level, 0, atten);
-        put(level, 1, prob);
-        put(level, 2, __int_as_float(mtl));
-    }
-    __device__ __forceinline__ void put_dst(int level, V3 dst) {
-        put(level, 3, dst.x);
-        if (words > 4) {
-            put(level, 4, dst.y);
-            put(level, 5, dst.z);
+    // mk = material id | p-kind << 30; probe = material the probe hit (kNoProbe: none)
+    __device__ __forceinline__ void put_dst(int level, uint32_t mk, uint32_t probe, V3 dst) {
+        if (words == 2) {
+            put(level, 1, __uint_as_float(mk | (probe << 15)));
+        } else {
+            put(level, 1, __uint_as_float(mk));
+            put(level, 2, dst.x);
+            put(level, 3, dst.y);
+            put(level, 4, dst.z);
         }
     }
 };
@@ -329,7 +403,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     PathRecords<MAXD> rec;
     rec.lds = (float*)(lds + a.lds_rec_offset) + tid;
     rec.nlds = a.rec_lds_levels;
-    rec.words = a.n_lights > 0 ? 6 : 4;
+    rec.words = rec_words(a.n_lights, a.n_materials);
 
     uint32_t st[6];
     V3 total = v3(0.0f, 0.0f, 0.0f);
@@ -340,7 +414,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     }
     int remaining = a.samples;
     int phase = PH_CAMERA;
-    int depth = 0, li = 0, mtl = 0;
+    int depth = 0, li = 0;
+    uint32_t mk = 0;   // material id | p-kind << 30 of the current bounce
     V3 rd = v3(0.0f, 0.0f, 0.0f), nd = rd, nrm = rd, direct = rd;
     Trav r;
     trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), false);
@@ -364,12 +439,12 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (r.u * v3(s1.x, s1.y, s1.z))) +
                                     (r.v * v3(s2.x, s2.y, s2.z)));
                     r.o = r.o + (r.t * rd);
-                    mtl = __float_as_int(s0.w);
-                    const float4 m0 = a.mtl[2 * mtl], m1 = a.mtl[2 * mtl + 1];
+                    const int mtl = __float_as_int(s0.w);
+                    const float4 m1 = a.mtl[2 * mtl + 1];
                     float af;
                     const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
-                    (void)m0;
-                    rec.put_shade(depth, af, prob, mtl);
+                    rec.put(depth, 0, af);
+                    mk = (uint32_t)mtl | (p_kind(prob) << 30);
                     direct = v3(0.0f, 0.0f, 0.0f);
                     li = 0;
                     lights_next = true;
@@ -378,25 +453,26 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 if (r.fid < 0) {   // sampleDeltaLights :279-282 (light re-sampled: deterministic)
                     V3 ldir, lrad;
                     light_sample(a.lights, li, r.o, ldir, lrad);
-                    const float4 m0 = a.mtl[2 * mtl];
+                    const float4 m0 = a.mtl[2 * (mk & 0x3fffffffu)];
                     direct = direct + (v3(m0.x, m0.y, m0.z) * lrad);
                 }
                 ++li;
                 lights_next = true;
             } else if (phase == PH_PROBE) {   // :390-400
                 V3 dl = direct;
+                uint32_t pm = kNoProbe;
                 if (r.fid >= 0) {
-                    const int pm = __float_as_int(a.shade[3 * r.fid].w);
+                    pm = (uint32_t)__float_as_int(a.shade[3 * r.fid].w);
                     const float e = a.mtl[2 * pm].w;
                     dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + direct;
                 }
-                rec.put_dst(depth, dl);
+                rec.put_dst(depth, mk, pm, dl);
                 after = true;
             }
             V3 td = rd;
             bool shadow = false;
             if (lights_next) {
-                const float4 m1 = a.mtl[2 * mtl + 1];
+                const float4 m1 = a.mtl[2 * (mk & 0x3fffffffu) + 1];
                 if (li < a.n_lights) {
                     V3 lrad;
                     light_sample(a.lights, li, r.o, td, lrad);
@@ -407,12 +483,12 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
                     phase = PH_PROBE;
                 } else {
-                    rec.put_dst(depth, direct);
+                    rec.put_dst(depth, mk, kNoProbe, direct);
                     after = true;
                 }
             }
             if (after) {
-                const float e = a.mtl[2 * mtl].w;
+                const float e = a.mtl[2 * (mk & 0x3fffffffu)].w;
                 if (e > 0.0f) {   // an emitter ends the path (:408-412); the unwind starts from e
                     L = e * v3(1.0f, 1.0f, 1.0f);
                     finish = true;
@@ -426,11 +502,23 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             }
             if (finish) {   // unwind (:416-431): levels depth-1 .. 0
                 for (int k = depth - 1; k >= 0; --k) {
-                    const float4 mb = a.mtl[2 * __float_as_int(rec.get(k, 2))];
-                    const V3 att = rec.get(k, 0) * v3(mb.x, mb.y, mb.z);       // :379
-                    const float ivp = 1.0f / rec.get(k, 1);                     // :427 "/ pStack"
-                    const float d0 = rec.get(k, 3);
-                    const V3 dst = rec.words > 4 ? v3(d0, rec.get(k, 4), rec.get(k, 5)) : v3(d0, d0, d0);
+                    const float af = rec.get(k, 0);
+                    const uint32_t w1 = __float_as_uint(rec.get(k, 1));
+                    const bool packed = rec.words == 2;
+                    const float4 mb = a.mtl[2 * (w1 & (packed ? 0x7fffu : 0x3fffffffu))];
+                    const V3 att = af * v3(mb.x, mb.y, mb.z);                   // :379
+                    const uint32_t kind = w1 >> 30;
+                    const float prob = kind == 0u ? af : (kind == 1u ? -0.0f : 0.0f);
+                    const float ivp = 1.0f / prob;                              // :427 "/ pStack"
+                    V3 dst;
+                    if (packed) {
+                        const uint32_t pm = (w1 >> 15) & 0x7fffu;
+                        const float e = pm == kNoProbe ? 0.0f : a.mtl[2 * pm].w;
+                        dst = pm == kNoProbe ? v3(0.0f, 0.0f, 0.0f)
+                                             : (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + v3(0.0f, 0.0f, 0.0f);
+                    } else {
+                        dst = v3(rec.get(k, 2), rec.get(k, 3), rec.get(k, 4));
+                    }
                     L = ivp * ((dst + L) * att);
                 }
                 total = total + L;
@@ -473,10 +561,65 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             const int cnt = __popcll(__ballot(ts == TS_TRAV));
             if (cnt == 0) break;
             if (cnt < refill && __ballot(ts == TS_DONE) != 0ull) break;
+#if TPT_LEAF_SPEC
+            // Speculative leaf postponement: a lane that reaches a leaf parks it
+            // (one slot) and keeps walking inner nodes; the wave runs the
+            // triangle branch only when enough lanes hold a parked leaf, when
+            // lanes are blocked (a second leaf, or nothing left but the parked
+            // one), or when no lane has inner work.  Leaves are still tested in
+            // the order the traversal reaches them; a stale r.t only weakens
+            // the ordered culling, and the ordered winner (least t, then
+            // largest leaf position) does not depend on test order.
+            bool inner_ready = false, has = false, blocked = false;
+            const bool at_inner = ts == TS_TRAV && r.node >= 0 && r.node < nint;
+            const bool minmax = ORDERED && a.boxes_finite && __ballot(at_inner && !r.fin) == 0ull;
+            if (ts == TS_TRAV) {
+                if (at_inner) {
+                    ++c_inner;
+                    int next, deferred;
+                    bool push;
+                    if (minmax) inner_visit_fast(r, a.inner, next, push, deferred);
+                    else inner_visit<ORDERED>(r, a.inner, next, push, deferred);
+                    if (push) {
+                        stk[r.sp * 256] = (StackT)deferred;
+                        if (r.sp >= a.stack_depth) {
+                            ++c_ovf;
+                            r.sp = 0;
+                            next = -1;
+                        } else {
+                            ++r.sp;
+                        }
+                    }
+                    r.node = next >= 0 ? next : (r.sp == 0 ? -1 : (int)stk[(--r.sp) * 256]);
+                }
+                if (r.node >= nint && r.pend < 0) {
+                    r.pend = r.node - nint;
+                    r.node = r.sp == 0 ? -1 : (int)stk[(--r.sp) * 256];
+                }
+                has = r.pend >= 0;
+                inner_ready = r.node >= 0 && r.node < nint;
+                blocked = has && !inner_ready;
+            }
+            const unsigned long long hb = __ballot(has);
+            if (hb != 0ull) {
+                const bool go = __popcll(__ballot(blocked)) >= TPT_LEAF_KB || __popcll(hb) >= TPT_LEAF_KP ||
+                                __ballot(inner_ready) == 0ull;
+                if (go && has) {
+                    ++c_leaf;
+                    if (leaf_test<ORDERED>(r, a.tri, r.pend)) {
+                        r.node = -1;
+                        r.sp = 0;
+                    }
+                    r.pend = -1;
+                }
+            }
+            if (ts == TS_TRAV && r.node < 0 && r.pend < 0) ts = TS_DONE;
+#else
             if (ts == TS_TRAV) {
                 if (!trav_step<ORDERED>(r, a.inner, a.tri, nint, stk, a.stack_depth, c_inner, c_leaf, c_ovf))
                     ts = TS_DONE;
             }
+#endif
         }
     }
     if (active) {
@@ -561,7 +704,7 @@ constexpr size_t kLdsBudget = 32768;
 size_t trace_lds_bytes(TraceArgs& a) {
     const size_t elem = (2 * (size_t)a.n_faces - 1) <= 65535 ? 2 : 4;
     const size_t stack = ((size_t)(a.stack_depth + 1) * 256 * elem + 15) / 16 * 16;
-    const size_t level = (a.n_lights > 0 ? 6 : 4) * 256 * sizeof(float);
+    const size_t level = (size_t)rec_words(a.n_lights, a.n_materials) * 256 * sizeof(float);
     size_t levels = stack < kLdsBudget ? (kLdsBudget - stack) / level : 0;
     if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;
     a.lds_rec_offset = (int)stack;
