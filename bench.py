@@ -28,10 +28,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
-# algorithmic bytes: internal visit = links 8 + 2 child AABBs 48;
-# leaf = fid 4 + 3 indices 12 + 3 vertices 36; shading hit = 3 normals 36 +
-# 3 indices 12 + material 60; pixel write = 12
-B_INNER, B_LEAF, B_HIT, B_PIX = 56, 52, 108, 12
+# algorithmic bytes: binary internal visit = links 8 + 2 child
+# AABBs 48; 4-wide visit = links 16 + 4 child AABBs 96; leaf = fid 4 + 3
+# indices 12 + 3 vertices 36; shading hit = 3 normals 36 + 3 indices 12 +
+# material 60; pixel write = 12
+B_INNER, B_WIDE, B_LEAF, B_HIT, B_PIX = 56, 112, 52, 108, 12
 
 
 def parse():
@@ -143,7 +144,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
-    keys = ["traversals", "internal_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
+    keys = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
             "rng_init_ms", "resolve_ms", "trace_launches"]
     local_tot = {k: float(sum(s[k] for s in stats)) for k in keys}
     vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64, device=f"cuda:{dev}")
@@ -167,17 +168,25 @@ def main():
         # roofline of the dominant kernel (k_trace), per launch, rank 0's device
         l_tot = local_tot
         nl = max(l_tot["trace_launches"], 1.0)
-        bytes_total = (B_INNER * l_tot["internal_visits"] + B_LEAF * l_tot["leaf_tests"] +
+        bytes_total = (B_INNER * l_tot["internal_visits"] + B_WIDE * l_tot["wide_visits"] + B_LEAF * l_tot["leaf_tests"] +
                        B_HIT * l_tot["shade_hits"] + B_PIX * l_tot["pixels"])
         bytes_per_launch = bytes_total / nl
         avg_launch_s = (l_tot["trace_ms"] / nl) / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
+        config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}",
+                  "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
+                  "max_depth": args.depth, "seed": args.seed,
+                  "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + RCCL gather"
+                  if world > 1 else "1 GPU"}
         if os.path.exists(args.pmc_json):
             try:
                 with open(args.pmc_json) as f:
                     pm = json.load(f)
-                traffic = pm.get("hbm_bytes_per_launch")
+                # PMC bytes are per launch of the profiled workload: use them
+                # only when that was this exact single-GPU configuration
+                if pm.get("bench_config") == config and pm.get("n_gpus") == world:
+                    traffic = pm.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         out = {
@@ -193,11 +202,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "reference asset input/box.gltf (tests/golden/scenes), seed 42, no env map (black miss)",
-            "config": {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}",
-                       "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
-                       "max_depth": args.depth, "seed": args.seed,
-                       "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + RCCL gather"
-                       if world > 1 else "1 GPU"},
+            "config": config,
             "msamples_per_s": round(tot["samples"] / elapsed / 1e6, 2),
             "rays_per_sample": round(rays / max(tot["samples"], 1), 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -100,7 +100,7 @@ typedef struct {
 
 typedef struct {
     uint64_t traversals;          /* traverseBVH calls: primary+extension+probe+shadow */
-    uint64_t internal_visits;     /* internal nodes popped */
+    uint64_t internal_visits;     /* binary internal nodes popped (reference-order / non-finite rays) */
     uint64_t leaf_tests;          /* leaves popped (triangle tests) */
     uint64_t shade_hits;          /* extension-ray hits shaded */
     uint64_t pixels;              /* pixels rendered by this call */
@@ -111,6 +111,7 @@ typedef struct {
     double total_ms;              /* whole tpt_render, host wall */
     int32_t trace_launches;
     int32_t pad;
+    uint64_t wide_visits;         /* 4-wide internal nodes popped (ordered traversal) */
 } tpt_stats;
 
 typedef struct tpt_scene tpt_scene;

@@ -60,7 +60,8 @@ class Stats(C.Structure):
     _fields_ = [("traversals", C.c_uint64), ("internal_visits", C.c_uint64), ("leaf_tests", C.c_uint64),
                 ("shade_hits", C.c_uint64), ("pixels", C.c_uint64), ("samples", C.c_uint64),
                 ("rng_init_ms", C.c_double), ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
-                ("total_ms", C.c_double), ("trace_launches", C.c_int32), ("pad", C.c_int32)]
+                ("total_ms", C.c_double), ("trace_launches", C.c_int32), ("pad", C.c_int32),
+                ("wide_visits", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}

@@ -6,6 +6,10 @@
 //       q2 = (R.min.z, R.max.xyz)  q3 = (bits(left), bits(right), 0, 0)
 //     child ids use the reference numbering (bvh.cu:164-214): id >= F-1 is
 //     the leaf at sorted position id-(F-1).
+//   inner4[8*(F-1)] float4  4-wide view for the ordered traversal: slot i is
+//     filled for internal node i at even depth and holds its up to 4
+//     grandchildren (a leaf child stands for itself): child k box = floats
+//     6k..6k+5 of q0..q5 (min.xyz, max.xyz), q6 = child ids (-1: none).
 //   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
 //   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, 0), (n2.xyz, 0)
 //   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)
@@ -33,6 +37,7 @@ constexpr int kJumpWords = 160 * 5;      // one 160x160 GF(2) matrix
 struct TraceArgs {
     // scene
     const float4* inner;
+    const float4* inner4;
     const float4* tri;
     const float4* shade;
     const float4* mtl;
@@ -63,7 +68,7 @@ struct TraceArgs {
     // per-pixel state (SoA over W*H pixels)
     uint32_t* rng;                       // 6 planes: v0..v4, d
     float* accum;                        // 3 planes: r, g, b (running totalRad)
-    unsigned long long* counters;        // [0] trav [1] inner [2] leaf [3] shade [4] overflow
+    unsigned long long* counters;        // [0] trav [1] inner [2] leaf [3] shade [4] overflow [5] wide
 };
 
 // Path-record words per bounce (k_trace): 2 when the scene has no delta lights
@@ -116,6 +121,7 @@ struct BuildBuffers {
     size_t sort_tmp_bytes;
     // outputs
     float4* inner;
+    float4* inner4;
     float4* tri;
     float4* shade;
     void* nodes36;                       // reference layout (2F-1) * 36 B

@@ -134,7 +134,7 @@ struct tpt_scene {
     DevBuf<uint32_t> fids, fids_sorted, parent, flags, max_depth;
     DevBuf<int2> children;
     DevBuf<uint8_t> sort_tmp, nodes36;
-    DevBuf<float4> inner, tri, shade;
+    DevBuf<float4> inner, inner4, tri, shade;
     // frame state
     DevBuf<uint32_t> rng;
     DevBuf<float> accum, radiance_tmp;
@@ -261,6 +261,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     HIP_OR_FAIL(s->max_depth.alloc(2));
     HIP_OR_FAIL(s->sort_tmp.alloc(std::max<size_t>(sort_bytes, 16)));
     HIP_OR_FAIL(s->inner.alloc(4 * std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->inner4.alloc(8 * std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->tri.alloc(3 * n));
     HIP_OR_FAIL(s->shade.alloc(3 * n));
     HIP_OR_FAIL(s->nodes36.alloc(36 * nn));
@@ -293,14 +294,18 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     b.sort_tmp = s->sort_tmp.p;
     b.sort_tmp_bytes = sort_bytes;
     b.inner = s->inner.p;
+    b.inner4 = s->inner4.p;
     b.tri = s->tri.p;
     b.shade = s->shade.p;
     b.nodes36 = s->nodes36.p;
     HIP_OR_FAIL(tpt::launch_build(b, s->stream));
     s->tree_depth = b.out_max_depth;
     s->boxes_finite = (int32_t)b.out_boxes_finite;
-    // DFS that pushes both children holds at most depth + 1 entries
-    s->stack_depth = (int32_t)std::max<uint32_t>(b.out_max_depth + 2, 2);
+    // Stack capacity: the binary DFS that pushes one sibling per level holds at
+    // most depth + 1 entries; the 4-wide ordered traversal pushes up to 3 per
+    // 4-wide node, one per two levels: 3 * ceil(depth / 2).
+    const uint32_t td = b.out_max_depth;
+    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, 3 * ((td + 1) / 2) + 1), 2);
     if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
     s->built = true;
     return TPT_OK;
@@ -338,6 +343,7 @@ void tpt_env_destroy(tpt_env* env) {
 
 static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, tpt::TraceArgs& a) {
     a.inner = s->inner.p;
+    a.inner4 = s->inner4.p;
     a.tri = s->tri.p;
     a.shade = s->shade.p;
     a.mtl = s->mtl.p;
@@ -484,6 +490,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
         std::memset(stats, 0, sizeof *stats);
         stats->traversals = cnt[0];
         stats->internal_visits = cnt[1];
+        stats->wide_visits = cnt[5];
         stats->leaf_tests = cnt[2];
         stats->shade_hits = cnt[3];
         stats->pixels = (uint64_t)W * (uint64_t)bh;

@@ -198,6 +198,41 @@ __global__ void k_pack_inner(BuildBuffers b) {
     if (!fin) atomicOr(b.max_depth + 1, 1u);
 }
 
+// 4-wide nodes for even-depth internal nodes: the children of a kept node's
+// internal children are themselves kept (depth + 2), so depth parity decides.
+__global__ void k_pack_inner4(BuildBuffers b, const uint32_t* __restrict__ depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nint = b.n_faces - 1;
+    if (i >= nint || (depth[i] & 1u)) return;
+    const int2 c = b.children[i];
+    int ids[4] = {-1, -1, -1, -1};
+    int n = 0;
+    const int cs[2] = {c.x, c.y};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (cs[h] >= nint) {
+            ids[n++] = cs[h];
+        } else {
+            const int2 g = b.children[cs[h]];
+            ids[n++] = g.x;
+            ids[n++] = g.y;
+        }
+    }
+    float f[24];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float* bx = b.node_box + 6 * (ids[k] < 0 ? 0 : ids[k]);
+#pragma unroll
+        for (int j = 0; j < 6; ++j) f[6 * k + j] = ids[k] < 0 ? 0.0f : bx[j];
+    }
+    float4* q = b.inner4 + 8 * i;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) q[k] = make_float4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
+    q[6] = make_float4(__int_as_float(ids[0]), __int_as_float(ids[1]), __int_as_float(ids[2]),
+                       __int_as_float(ids[3]));
+    q[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
 __global__ void k_pack_leaf(BuildBuffers b) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = b.n_faces;
@@ -291,6 +326,8 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s) {
     }
     if (n > 1) {
         hipLaunchKernelGGL(k_pack_inner, grid(n - 1), blk, 0, s, b);
+        TPT_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_pack_inner4, grid(n - 1), blk, 0, s, b, depth);
         TPT_TRY(hipGetLastError());
     }
     hipLaunchKernelGGL(k_pack_leaf, grid(n), blk, 0, s, b);

@@ -99,7 +99,7 @@ struct Trav {
     bool fin;   // origin and 1/dir finite: no slab product can be NaN
 };
 
-__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
+__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit, bool boxes_finite = false) {
     r.o = o;
     r.d = d;
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
@@ -112,7 +112,7 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit) {
     r.u = 0.0f;
     r.v = 0.0f;
     r.any_hit = any_hit;
-    r.fin = __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
+    r.fin = boxes_finite & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
             __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
 }
 
@@ -171,6 +171,66 @@ __device__ __forceinline__ void inner_visit_fast(const Trav& r, const float4* __
     push = hl & hr;
     deferred = lfirst ? rc : lc;
     next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
+}
+
+// 4-wide visit (ordered traversal, finite rays and boxes): tests the up to 4
+// grandchildren of node r.node (inner4 layout, device_api.hpp) with the
+// min/max slab test.  A grandchild's box lies inside its parent's (exact
+// min/max unions) and the slab arithmetic is monotonic in the bounds, so a
+// grandchild that passes implies its parent passes: the set of leaves reached
+// is the binary traversal's.  Hit children are sorted by slab entry; the
+// nearest is returned, the others (up to 3) are pushed farthest-first.  The
+// stack region has 3 spare slots so all three writes are unconditional.
+template <typename StackT>
+__device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4, StackT* stk,
+                                            int& sp) {
+    const float4* nd = inner4 + 8 * r.node;
+    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
+    float k0, k1, k2, k3, e0, e1, e2, e3;
+    slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
+    slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
+    slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
+    slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
+    const float hi = fminf(kRealMax, r.t * 1.0001f);
+    int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z), i3 = __float_as_int(q6.w);
+    const float hd = 0.5f * kDelta;
+    const bool h0 = (i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi));
+    const bool h1 = (i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi));
+    const bool h2 = (i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi));
+    const bool h3 = (i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi));
+    const float inf = __builtin_inff();
+    k0 = h0 ? k0 : inf;
+    k1 = h1 ? k1 : inf;
+    k2 = h2 ? k2 : inf;
+    k3 = h3 ? k3 : inf;
+    i0 = h0 ? i0 : -1;
+    i1 = h1 ? i1 : -1;
+    i2 = h2 ? i2 : -1;
+    i3 = h3 ? i3 : -1;
+    const int m = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+#define TPT_CX(ka, ia, kb, ib)          \
+    {                                   \
+        const bool sw = kb < ka;        \
+        const float tk = sw ? kb : ka;  \
+        kb = sw ? ka : kb;              \
+        ka = tk;                        \
+        const int ti = sw ? ib : ia;    \
+        ib = sw ? ia : ib;              \
+        ia = ti;                        \
+    }
+    TPT_CX(k0, i0, k1, i1)
+    TPT_CX(k2, i2, k3, i3)
+    TPT_CX(k0, i0, k2, i2)
+    TPT_CX(k1, i1, k3, i3)
+    TPT_CX(k1, i1, k2, i2)
+#undef TPT_CX
+    // push sorted[m-1] .. sorted[1] (m-1 entries), farthest at the bottom
+    const int np = m > 0 ? m - 1 : 0;
+    stk[sp * 256] = (StackT)(np == 3 ? i3 : (np == 2 ? i2 : i1));
+    stk[(sp + 1) * 256] = (StackT)(np == 3 ? i2 : i1);
+    stk[(sp + 2) * 256] = (StackT)i1;
+    sp += np;
+    return i0;   // -1 when no child was entered
 }
 
 // rayHitTriangle (geometry_queries.h:65-86) on leaf position pos, e1/e2
@@ -395,7 +455,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
     const bool active = x < a.width && ly < a.band_height && y < a.height;
-    uint32_t c_trav = 0, c_inner = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
+    uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
     const int nint = a.n_faces - 1;
@@ -551,7 +611,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             }
             if (ts != TS_DEAD) {
                 ++c_trav;
-                trav_begin(r, to, td, shadow);
+                trav_begin(r, to, td, shadow, a.boxes_finite != 0);
                 ts = TS_TRAV;
             }
         }
@@ -572,23 +632,24 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             // largest leaf position) does not depend on test order.
             bool inner_ready = false, has = false, blocked = false;
             const bool at_inner = ts == TS_TRAV && r.node >= 0 && r.node < nint;
-            const bool minmax = ORDERED && a.boxes_finite && __ballot(at_inner && !r.fin) == 0ull;
             if (ts == TS_TRAV) {
                 if (at_inner) {
-                    ++c_inner;
-                    int next, deferred;
-                    bool push;
-                    if (minmax) inner_visit_fast(r, a.inner, next, push, deferred);
-                    else inner_visit<ORDERED>(r, a.inner, next, push, deferred);
-                    if (push) {
+                    int next;
+                    if (ORDERED && r.fin) {   // 4-wide (r.fin includes a.boxes_finite)
+                        ++c_wide;
+                        next = inner_visit4(r, a.inner4, stk, r.sp);
+                    } else {                  // binary, the reference's exact slab test
+                        ++c_inner;
+                        int deferred;
+                        bool push;
+                        inner_visit<ORDERED>(r, a.inner, next, push, deferred);
                         stk[r.sp * 256] = (StackT)deferred;
-                        if (r.sp >= a.stack_depth) {
-                            ++c_ovf;
-                            r.sp = 0;
-                            next = -1;
-                        } else {
-                            ++r.sp;
-                        }
+                        r.sp += push ? 1 : 0;
+                    }
+                    if (r.sp > a.stack_depth) {
+                        ++c_ovf;
+                        r.sp = 0;
+                        next = -1;
                     }
                     r.node = next >= 0 ? next : (r.sp == 0 ? -1 : (int)stk[(--r.sp) * 256]);
                 }
@@ -629,6 +690,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         a.accum[npix + off] = total.y;
         a.accum[2 * npix + off] = total.z;
     }
+    const unsigned long long s_wide = wave_sum(c_wide);
     const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
                              s_shade = wave_sum(c_shade), s_ovf = wave_sum(c_ovf);
     if (lane == 0) {
@@ -637,6 +699,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[2], s_leaf);
         atomicAdd(&a.counters[3], s_shade);
         if (s_ovf) atomicAdd(&a.counters[4], s_ovf);
+        atomicAdd(&a.counters[5], s_wide);
     }
 }
 
@@ -698,12 +761,13 @@ static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_
 }
 
 // LDS per 256-lane workgroup: the traversal stack, then as many path-record
-// levels as fit in kLdsBudget (5 workgroups per CU share the 160 KiB).
-constexpr size_t kLdsBudget = 32768;
+// levels as fit in kLdsBudget (TPT_TRACE_WAVES workgroups per CU share the
+// 160 KiB).
+constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
 
 size_t trace_lds_bytes(TraceArgs& a) {
     const size_t elem = (2 * (size_t)a.n_faces - 1) <= 65535 ? 2 : 4;
-    const size_t stack = ((size_t)(a.stack_depth + 1) * 256 * elem + 15) / 16 * 16;
+    const size_t stack = ((size_t)(a.stack_depth + 3) * 256 * elem + 15) / 16 * 16;
     const size_t level = (size_t)rec_words(a.n_lights, a.n_materials) * 256 * sizeof(float);
     size_t levels = stack < kLdsBudget ? (kLdsBudget - stack) / level : 0;
     if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;

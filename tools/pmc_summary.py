@@ -43,6 +43,19 @@ if "FETCH_SIZE" in p or "WRITE_SIZE" in p:
     s["fetch_bytes_raw"] = fetch
     s["write_bytes"] = write
     s["hbm_bytes_per_launch"] = 2.0 * fetch + write
+# the bench line printed under the kernel-trace pass names the profiled workload
+try:
+    with open(os.path.join(out_dir, "ktrace.log")) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("{") and '"metric"' in line:
+                b = json.loads(line)
+                s["bench_config"] = b.get("config")
+                s["n_gpus"] = b.get("n_gpus")
+                s["bench_value"] = b.get("value")
+                s["launches_per_step"] = b.get("roofline", {}).get("launches_per_step")
+except OSError:
+    pass
 if p.get("GRBM_GUI_ACTIVE") and s.get("avg_duration_ms"):
     s["effective_clock_ghz"] = p["GRBM_GUI_ACTIVE"] / 8.0 / (s["avg_duration_ms"] * 1e6)
 print(json.dumps(s, indent=1))

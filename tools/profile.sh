@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
-ARGS=${@:---spp 64 --steps 1 --warmup 0 --cpu-baseline 0}
+ARGS=${@:---steps 1 --warmup 0 --cpu-baseline 0}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ktrace -o run --output-format csv -- python3 bench.py $ARGS > $OUT/ktrace.log 2>&1 || exit 1
