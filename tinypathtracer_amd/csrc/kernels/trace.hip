@@ -447,7 +447,10 @@ struct PathRecords {
     }
 };
 
-template <int MAXD, bool ORDERED, typename StackT>
+// LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
+// state (direct term, normal, light index, incoming direction -- r.d during an
+// extension ray) is dead across traversals and drops out of the registers.
+template <int MAXD, bool ORDERED, bool LIGHTS, typename StackT>
 __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -463,7 +466,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     PathRecords<MAXD> rec;
     rec.lds = (float*)(lds + a.lds_rec_offset) + tid;
     rec.nlds = a.rec_lds_levels;
-    rec.words = rec_words(a.n_lights, a.n_materials);
+    rec.words = LIGHTS ? 5 : 2;
 
     uint32_t st[6];
     V3 total = v3(0.0f, 0.0f, 0.0f);
@@ -487,6 +490,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
             V3 L = v3(0.0f, 0.0f, 0.0f);
+            if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
             if (phase == PH_EXT) {
                 if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
                     if (a.env) L = env_lookup(a.env, a.env_w, a.env_h, rd);
@@ -509,7 +513,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     li = 0;
                     lights_next = true;
                 }
-            } else if (phase == PH_SHADOW) {
+            } else if (LIGHTS && phase == PH_SHADOW) {
                 if (r.fid < 0) {   // sampleDeltaLights :279-282 (light re-sampled: deterministic)
                     V3 ldir, lrad;
                     light_sample(a.lights, li, r.o, ldir, lrad);
@@ -519,12 +523,12 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 ++li;
                 lights_next = true;
             } else if (phase == PH_PROBE) {   // :390-400
-                V3 dl = direct;
+                V3 dl = LIGHTS ? direct : v3(0.0f, 0.0f, 0.0f);
                 uint32_t pm = kNoProbe;
                 if (r.fid >= 0) {
                     pm = (uint32_t)__float_as_int(a.shade[3 * r.fid].w);
                     const float e = a.mtl[2 * pm].w;
-                    dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + direct;
+                    dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + dl;
                 }
                 rec.put_dst(depth, mk, pm, dl);
                 after = true;
@@ -533,7 +537,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             bool shadow = false;
             if (lights_next) {
                 const float4 m1 = a.mtl[2 * (mk & 0x3fffffffu) + 1];
-                if (li < a.n_lights) {
+                if (LIGHTS && li < a.n_lights) {
                     V3 lrad;
                     light_sample(a.lights, li, r.o, td, lrad);
                     phase = PH_SHADOW;
@@ -748,16 +752,25 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
     }
 }
 
-template <bool ORDERED, typename StackT>
+template <bool ORDERED, bool LIGHTS, typename StackT>
 static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     if (a.max_depth <= 8)
-        hipLaunchKernelGGL((k_trace<8, ORDERED, StackT>), grid, dim3(256), lds, s, a);
-    else if (a.max_depth <= 16)
-        hipLaunchKernelGGL((k_trace<16, ORDERED, StackT>), grid, dim3(256), lds, s, a);
-    else if (a.max_depth <= 32)
-        hipLaunchKernelGGL((k_trace<32, ORDERED, StackT>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_trace<8, ORDERED, LIGHTS, StackT>), grid, dim3(256), lds, s, a);
     else
-        hipLaunchKernelGGL((k_trace<64, ORDERED, StackT>), grid, dim3(256), lds, s, a);
+        hipLaunchKernelGGL((k_trace<64, ORDERED, LIGHTS, StackT>), grid, dim3(256), lds, s, a);
+}
+
+template <bool ORDERED>
+static void launch_trace_o(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
+    const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
+    if (lights) {
+        if (small) launch_trace_t<ORDERED, true, uint16_t>(a, grid, lds, s);
+        else launch_trace_t<ORDERED, true, int>(a, grid, lds, s);
+    } else {
+        if (small) launch_trace_t<ORDERED, false, uint16_t>(a, grid, lds, s);
+        else launch_trace_t<ORDERED, false, int>(a, grid, lds, s);
+    }
 }
 
 // LDS per 256-lane workgroup: the traversal stack, then as many path-record
@@ -780,14 +793,8 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
     const size_t lds = trace_lds_bytes(a);
     dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
-    const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
-    if (a.flags & TPT_FLAG_REF_ORDER) {
-        if (small) launch_trace_t<false, uint16_t>(a, grid, lds, s);
-        else launch_trace_t<false, int>(a, grid, lds, s);
-    } else {
-        if (small) launch_trace_t<true, uint16_t>(a, grid, lds, s);
-        else launch_trace_t<true, int>(a, grid, lds, s);
-    }
+    if (a.flags & TPT_FLAG_REF_ORDER) launch_trace_o<false>(a, grid, lds, s);
+    else launch_trace_o<true>(a, grid, lds, s);
     return hipGetLastError();
 }
 
