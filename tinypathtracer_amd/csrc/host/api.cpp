@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -392,9 +393,9 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
 
     HIP_OR_FAIL(s->rng.alloc(6 * npix));
     HIP_OR_FAIL(s->accum.alloc(3 * npix));
-    HIP_OR_FAIL(s->counters.alloc(8));
+    HIP_OR_FAIL(s->counters.alloc(16));
     HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * sizeof(float), st));   // thrust::fill (:534)
-    HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 8 * sizeof(unsigned long long), st));
+    HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 16 * sizeof(unsigned long long), st));
 
     // setupRandSeed (:513)
     HIP_OR_FAIL(hipEventRecord(s->ev[0], st));
@@ -482,10 +483,15 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
                                    st));
     if (bgra_out && !bgra_dev)
         HIP_OR_FAIL(hipMemcpyAsync(bgra_out, s->bgra_tmp.p, 4 * npix, hipMemcpyDeviceToHost, st));
-    unsigned long long cnt[8] = {0};
+    unsigned long long cnt[16] = {0};
     HIP_OR_FAIL(hipMemcpyAsync(cnt, s->counters.p, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
     if (cnt[4] != 0) return fail(TPT_ERR_HIP, "traversal stack overflow (BVH deeper than sized)");
+    if (std::getenv("TPT_DEBUG_COUNTERS")) {   // raw kernel counters (phase-profiling builds fill 6..8)
+        std::fprintf(stderr, "tpt counters:");
+        for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %llu", cnt[i]);
+        std::fprintf(stderr, "\n");
+    }
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         stats->traversals = cnt[0];

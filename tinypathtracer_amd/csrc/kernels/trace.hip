@@ -485,7 +485,18 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     int ts = active ? TS_DONE : TS_DEAD;
     const int refill = a.refill;
 
+#ifdef TPT_PROFILE_PHASES
+    unsigned long long p_done = 0, p_trav = 0, p_steps = 0, t_iter0 = 0, t_loop0 = 0, p_outer = 0;
+    unsigned long long p_sub[3] = {0, 0, 0};
+#endif
     for (;;) {
+#ifdef TPT_PROFILE_PHASES
+        {
+            const unsigned long long now = wall_clock64();
+            if (t_loop0) p_trav += now - t_loop0;   // the previous traversal loop
+            t_iter0 = now;
+        }
+#endif
         if (ts == TS_DONE) {
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
@@ -564,6 +575,10 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     else phase = PH_EXT;
                 }
             }
+#ifdef TPT_PROFILE_PHASES
+            unsigned long long t_a = wall_clock64();
+            p_sub[0] += t_a - t_iter0;
+#endif
             if (finish) {   // unwind (:416-431): levels depth-1 .. 0
                 for (int k = depth - 1; k >= 0; --k) {
                     const float af = rec.get(k, 0);
@@ -588,6 +603,13 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 total = total + L;
                 phase = PH_CAMERA;
             }
+#ifdef TPT_PROFILE_PHASES
+            {
+                const unsigned long long t_b = wall_clock64();
+                p_sub[1] += t_b - t_a;
+                t_a = t_b;
+            }
+#endif
             V3 to = r.o;
             if (phase == PH_CAMERA) {
                 if (remaining == 0) {
@@ -613,6 +635,12 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     phase = PH_EXT;
                 }
             }
+#ifdef TPT_PROFILE_PHASES
+            {
+                const unsigned long long t_b = wall_clock64();
+                p_sub[2] += t_b - t_a;
+            }
+#endif
             if (ts != TS_DEAD) {
                 ++c_trav;
                 trav_begin(r, to, td, shadow, a.boxes_finite != 0);
@@ -620,8 +648,16 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             }
         }
         if (__ballot(ts != TS_DEAD) == 0ull) break;
+#ifdef TPT_PROFILE_PHASES
+        t_loop0 = wall_clock64();
+        p_done += t_loop0 - t_iter0;
+        ++p_outer;
+#endif
         // ---- traversal: step while enough lanes of the wave are still traversing ----
         for (;;) {
+#ifdef TPT_PROFILE_PHASES
+            ++p_steps;
+#endif
             const int cnt = __popcll(__ballot(ts == TS_TRAV));
             if (cnt == 0) break;
             if (cnt < refill && __ballot(ts == TS_DONE) != 0ull) break;
@@ -704,6 +740,15 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[3], s_shade);
         if (s_ovf) atomicAdd(&a.counters[4], s_ovf);
         atomicAdd(&a.counters[5], s_wide);
+#ifdef TPT_PROFILE_PHASES
+        atomicAdd(&a.counters[6], p_done);
+        atomicAdd(&a.counters[7], p_trav);
+        atomicAdd(&a.counters[8], p_steps);
+        atomicAdd(&a.counters[9], p_sub[0]);
+        atomicAdd(&a.counters[10], p_sub[1]);
+        atomicAdd(&a.counters[11], p_sub[2]);
+        atomicAdd(&a.counters[12], p_outer);
+#endif
     }
 }
 
