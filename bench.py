@@ -40,7 +40,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", choices=sorted(PRESETS), default=None,
+                    help="SURVEY 8(d) preset; explicit flags after it still override")
     ap.add_argument("--scene", default="box")
+    ap.add_argument("--env", choices=["sky"], default=None, help="procedural equirect env on miss")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
@@ -55,14 +58,47 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_trace_latest.json"),
                     help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/profile.sh)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config:
+        # preset values, unless the flag was given explicitly on the command line
+        given = {a.split("=")[0].lstrip("-").replace("-", "_") for a in sys.argv[1:] if a.startswith("--")}
+        for k, v in PRESETS[args.config].items():
+            if k not in given:
+                setattr(args, k, v)
+    return args
+
+
+# SURVEY 8(d) configurations (C1 is the CPU-only case reported inside cpu_baseline)
+PRESETS = {
+    "C2": dict(scene="box", width=1920, height=1080, spp=1024, depth=8, env=None),
+    "C3": dict(scene="ball", width=1920, height=1080, spp=4096, depth=8, env="sky"),
+    "C4": dict(scene="tir", width=1920, height=1080, spp=8192, depth=32, env=None),
+    "C5": dict(scene="c5", width=3840, height=2160, spp=2048, depth=8, env=None),
+}
+SCENE_DIR = os.path.join(ROOT, "tests", "golden", "scenes")
 
 
 def scene_file(name):
-    p = os.path.join(ROOT, "tests", "golden", "scenes", f"{name}.gltf")
+    if name == "c5":   # synthesized from the shipped scenes (tinypathtracer_amd.synth)
+        import tempfile
+        from tinypathtracer_amd import synth
+        out = os.path.join(tempfile.gettempdir(), "tpt_scenes", "c5.gltf")
+        synth.write_c5(out, SCENE_DIR)
+        return out
+    p = os.path.join(SCENE_DIR, f"{name}.gltf")
     if not os.path.exists(p):
         p = name
     return p
+
+
+def data_note(args):
+    if args.scene == "c5":
+        src = "synthesized C5 scene (box+box1+box2+light, 3x midpoint subdivision, 131,712 triangles)"
+    else:
+        src = f"reference asset input/{args.scene}.gltf (tests/golden/scenes)"
+    env = "procedural 2048x1024 sky env (the reference's JPG is missing)" if args.env == "sky" \
+        else "no env map (black miss)"
+    return f"{src}, seed {args.seed}, {env}"
 
 
 def cpu_baseline(args):
@@ -117,6 +153,8 @@ def main():
     build_ms = (time.perf_counter() - t0) * 1e3
     W, H = args.width, args.height
     pt = T.PathTracer("", W, H, dev)
+    if args.env == "sky":
+        pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), device=dev)
     radiance = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
     band = (args.band_rows, world, rank)
 
@@ -174,7 +212,8 @@ def main():
         avg_launch_s = (l_tot["trace_ms"] / nl) / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
-        config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}",
+        config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}"
+                              + (" env sky" if args.env else ""),
                   "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
                   "max_depth": args.depth, "seed": args.seed,
                   "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + RCCL gather"
@@ -201,7 +240,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "reference asset input/box.gltf (tests/golden/scenes), seed 42, no env map (black miss)",
+            "data": data_note(args),
             "config": config,
             "msamples_per_s": round(tot["samples"] / elapsed / 1e6, 2),
             "rays_per_sample": round(rays / max(tot["samples"], 1), 4),

@@ -18,6 +18,14 @@ def pytest_configure(config):
 
 
 def scene_path(name):
+    """Shipped scenes from tests/golden/scenes; "c5" is synthesized from them
+    (tinypathtracer_amd.synth) into the temp dir once."""
+    if name == "c5":
+        import tempfile
+        from tinypathtracer_amd import synth
+        out = os.path.join(tempfile.gettempdir(), "tpt_scenes", "c5.gltf")
+        synth.write_c5(out, SCENE_DIR)
+        return out
     return os.path.join(SCENE_DIR, f"{name}.gltf")
 
 

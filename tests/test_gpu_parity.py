@@ -19,7 +19,7 @@ from tests.conftest import ROOT, scene_path
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["box", "box1", "box2", "ball", "tir", "light", "square"]
+SCENES = ["box", "box1", "box2", "ball", "tir", "light", "square", "c5"]
 
 
 def _bits(a):
@@ -142,6 +142,7 @@ CASES = [
     ("square", 64, 36, 16, 8, None),
     ("light", 64, 36, 8, 8, "sky"),
     ("box1", 40, 24, 8, 8, "sky"),
+    ("c5", 96, 54, 8, 8, None),   # 131,712 triangles: 32-bit stack ids, LDS + private stack
 ]
 
 

@@ -65,6 +65,7 @@ struct TraceArgs {
     int32_t boxes_finite;                // all node boxes finite: min/max slab test is exact
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
+    int32_t stack_lds_slots;             // set by launch_trace: stack slots held in LDS (rest private)
     // per-pixel state (SoA over W*H pixels)
     uint32_t* rng;                       // 6 planes: v0..v4, d
     float* accum;                        // 3 planes: r, g, b (running totalRad)

@@ -26,9 +26,6 @@
 #include "../common/tpt_math.hpp"
 #include "tpt.h"
 
-#ifndef TPT_LEAF_SPEC
-#define TPT_LEAF_SPEC 1   // speculative leaf postponement (k_trace)
-#endif
 #ifndef TPT_LEAF_KB
 #define TPT_LEAF_KB 8     // run the triangle branch once this many lanes are blocked ...
 #endif
@@ -173,6 +170,25 @@ __device__ __forceinline__ void inner_visit_fast(const Trav& r, const float4* __
     next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
 }
 
+// Traversal stack of one lane: slots [0, nlds) in LDS ([slot][lane], shared
+// memory of the workgroup), deeper slots in private memory.  Deep stacks are
+// rare (the ordered traversal keeps few deferred siblings), so scenes whose
+// worst-case capacity exceeds the LDS budget (large trees, 32-bit ids) keep
+// the LDS fast path for all but the deepest moments.
+constexpr int kMaxStackSlots = 160 + 3;
+
+template <typename StackT>
+struct LaneStack {
+    StackT* lds;
+    int nlds;
+    StackT deep[kMaxStackSlots];
+    __device__ __forceinline__ void put(int i, int v) {
+        if (i < nlds) lds[i * 256] = (StackT)v;
+        else deep[i - nlds] = (StackT)v;
+    }
+    __device__ __forceinline__ int get(int i) const { return i < nlds ? (int)lds[i * 256] : (int)deep[i - nlds]; }
+};
+
 // 4-wide visit (ordered traversal, finite rays and boxes): tests the up to 4
 // grandchildren of node r.node (inner4 layout, device_api.hpp) with the
 // min/max slab test.  A grandchild's box lies inside its parent's (exact
@@ -182,7 +198,7 @@ __device__ __forceinline__ void inner_visit_fast(const Trav& r, const float4* __
 // nearest is returned, the others (up to 3) are pushed farthest-first.  The
 // stack region has 3 spare slots so all three writes are unconditional.
 template <typename StackT>
-__device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4, StackT* stk,
+__device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4, LaneStack<StackT>& stk,
                                             int& sp) {
     const float4* nd = inner4 + 8 * r.node;
     const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
@@ -226,9 +242,16 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
 #undef TPT_CX
     // push sorted[m-1] .. sorted[1] (m-1 entries), farthest at the bottom
     const int np = m > 0 ? m - 1 : 0;
-    stk[sp * 256] = (StackT)(np == 3 ? i3 : (np == 2 ? i2 : i1));
-    stk[(sp + 1) * 256] = (StackT)(np == 3 ? i2 : i1);
-    stk[(sp + 2) * 256] = (StackT)i1;
+    const int v0 = np == 3 ? i3 : (np == 2 ? i2 : i1), v1 = np == 3 ? i2 : i1;
+    if (sp + 3 <= stk.nlds) {
+        stk.lds[sp * 256] = (StackT)v0;
+        stk.lds[(sp + 1) * 256] = (StackT)v1;
+        stk.lds[(sp + 2) * 256] = (StackT)i1;
+    } else {
+        stk.put(sp, v0);
+        stk.put(sp + 1, v1);
+        stk.put(sp + 2, i1);
+    }
     sp += np;
     return i0;   // -1 when no child was entered
 }
@@ -462,7 +485,9 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
     const int nint = a.n_faces - 1;
-    StackT* stk = (StackT*)lds + tid;
+    LaneStack<StackT> stk;
+    stk.lds = (StackT*)lds + tid;
+    stk.nlds = a.stack_lds_slots;
     PathRecords<MAXD> rec;
     rec.lds = (float*)(lds + a.lds_rec_offset) + tid;
     rec.nlds = a.rec_lds_levels;
@@ -661,7 +686,6 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             const int cnt = __popcll(__ballot(ts == TS_TRAV));
             if (cnt == 0) break;
             if (cnt < refill && __ballot(ts == TS_DONE) != 0ull) break;
-#if TPT_LEAF_SPEC
             // Speculative leaf postponement: a lane that reaches a leaf parks it
             // (one slot) and keeps walking inner nodes; the wave runs the
             // triangle branch only when enough lanes hold a parked leaf, when
@@ -683,7 +707,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                         int deferred;
                         bool push;
                         inner_visit<ORDERED>(r, a.inner, next, push, deferred);
-                        stk[r.sp * 256] = (StackT)deferred;
+                        stk.put(r.sp, deferred);
                         r.sp += push ? 1 : 0;
                     }
                     if (r.sp > a.stack_depth) {
@@ -691,11 +715,11 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                         r.sp = 0;
                         next = -1;
                     }
-                    r.node = next >= 0 ? next : (r.sp == 0 ? -1 : (int)stk[(--r.sp) * 256]);
+                    r.node = next >= 0 ? next : (r.sp == 0 ? -1 : stk.get(--r.sp));
                 }
                 if (r.node >= nint && r.pend < 0) {
                     r.pend = r.node - nint;
-                    r.node = r.sp == 0 ? -1 : (int)stk[(--r.sp) * 256];
+                    r.node = r.sp == 0 ? -1 : stk.get(--r.sp);
                 }
                 has = r.pend >= 0;
                 inner_ready = r.node >= 0 && r.node < nint;
@@ -715,12 +739,6 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 }
             }
             if (ts == TS_TRAV && r.node < 0 && r.pend < 0) ts = TS_DONE;
-#else
-            if (ts == TS_TRAV) {
-                if (!trav_step<ORDERED>(r, a.inner, a.tri, nint, stk, a.stack_depth, c_inner, c_leaf, c_ovf))
-                    ts = TS_DONE;
-            }
-#endif
         }
     }
     if (active) {
@@ -825,10 +843,17 @@ constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
 
 size_t trace_lds_bytes(TraceArgs& a) {
     const size_t elem = (2 * (size_t)a.n_faces - 1) <= 65535 ? 2 : 4;
-    const size_t stack = ((size_t)(a.stack_depth + 3) * 256 * elem + 15) / 16 * 16;
+    const size_t slot = 256 * elem;
     const size_t level = (size_t)rec_words(a.n_lights, a.n_materials) * 256 * sizeof(float);
+    // Whole stack (capacity + 3 spare slots for the unconditional 4-wide
+    // pushes) in LDS when it leaves room for 2 record levels; otherwise the
+    // stack's first slots share the budget with 2 levels, the rest is private.
+    size_t slots = (size_t)a.stack_depth + 3;
+    if (slots * slot + 2 * level > kLdsBudget) slots = (kLdsBudget - 2 * level) / slot;
+    const size_t stack = (slots * slot + 15) / 16 * 16;
     size_t levels = stack < kLdsBudget ? (kLdsBudget - stack) / level : 0;
     if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;
+    a.stack_lds_slots = (int)slots;
     a.lds_rec_offset = (int)stack;
     a.rec_lds_levels = (int)levels;
     return stack + levels * level;
