@@ -43,7 +43,9 @@ def parse():
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="SURVEY 8(d) preset; explicit flags after it still override")
     ap.add_argument("--scene", default="box")
-    ap.add_argument("--env", choices=["sky"], default=None, help="procedural equirect env on miss")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="1-GPU rehearsal of an N-rank run: render only rank 0's bands of an N-way split")
+    ap.add_argument("--env", choices=["sky", "none"], default=None, help="procedural equirect env on miss")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
@@ -153,10 +155,14 @@ def main():
     build_ms = (time.perf_counter() - t0) * 1e3
     W, H = args.width, args.height
     pt = T.PathTracer("", W, H, dev)
+    if args.env == "none":
+        args.env = None
     if args.env == "sky":
         pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), device=dev)
     radiance = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
     band = (args.band_rows, world, rank)
+    if args.emulate_ranks > 1 and world == 1:
+        band = (args.band_rows, args.emulate_ranks, 0)
 
     def step():
         st = pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,

@@ -66,10 +66,14 @@ struct TraceArgs {
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
     int32_t stack_lds_slots;             // set by launch_trace: stack slots held in LDS (rest private)
+    int32_t lds_stack_offset;            // set by launch_trace: byte offset of the stack region
+    int32_t lds_mtl_offset;              // set by launch_trace: byte offset of the material table
+    int32_t mtl_in_lds;                  // set by launch_trace: material table copied to LDS
     // per-pixel state (SoA over W*H pixels)
     uint32_t* rng;                       // 6 planes: v0..v4, d
     float* accum;                        // 3 planes: r, g, b (running totalRad)
     unsigned long long* counters;        // [0] trav [1] inner [2] leaf [3] shade [4] overflow [5] wide
+    unsigned long long* debug_waves;     // phase-profiling builds: 8 words per wave (null: off)
 };
 
 // Path-record words per bounce (k_trace): 2 when the scene has no delta lights

@@ -140,7 +140,7 @@ struct tpt_scene {
     DevBuf<uint32_t> rng;
     DevBuf<float> accum, radiance_tmp;
     DevBuf<uint8_t> bgra_tmp;
-    DevBuf<unsigned long long> counters;
+    DevBuf<unsigned long long> counters, debug;
     size_t frame_pixels = 0;
 
     ~tpt_scene() {
@@ -420,6 +420,14 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;
+    a.debug_waves = nullptr;
+    const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");   // phase-profiling builds only
+    const size_t dbg_words = 8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 15) / 16);
+    if (dbg_path) {
+        HIP_OR_FAIL(s->debug.alloc(dbg_words));
+        HIP_OR_FAIL(hipMemsetAsync(s->debug.p, 0, dbg_words * sizeof(unsigned long long), st));
+        a.debug_waves = s->debug.p;
+    }
 
     int chunk = p->spp_per_launch;
     if (chunk <= 0) {
@@ -487,6 +495,14 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     HIP_OR_FAIL(hipMemcpyAsync(cnt, s->counters.p, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
     if (cnt[4] != 0) return fail(TPT_ERR_HIP, "traversal stack overflow (BVH deeper than sized)");
+    if (dbg_path) {
+        std::vector<unsigned long long> h(dbg_words);
+        HIP_OR_FAIL(hipMemcpy(h.data(), s->debug.p, dbg_words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        if (FILE* f = std::fopen(dbg_path, "wb")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+            std::fclose(f);
+        }
+    }
     if (std::getenv("TPT_DEBUG_COUNTERS")) {   // raw kernel counters (phase-profiling builds fill 6..8)
         std::fprintf(stderr, "tpt counters:");
         for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %llu", cnt[i]);

@@ -38,6 +38,14 @@
 
 namespace tpt {
 
+// LDS-typed pointers: the compiler then always emits ds_* accesses; a plain
+// (generic) pointer that may meet a private or global one in a select is
+// lowered to slower flat accesses.
+#define TPT_LDS __attribute__((address_space(3)))
+struct alignas(16) LdsF4 {   // float4 stand-in usable in LDS address space
+    float x, y, z, w;
+};
+
 // rayHitBBox (geometry_queries.h:18-46) with 1/dir hoisted per ray (same
 // values), written without branches: the reference returns false at the first
 // axis whose slab misses the running interval; a sticky `miss` flag gives the
@@ -179,7 +187,7 @@ constexpr int kMaxStackSlots = 160 + 3;
 
 template <typename StackT>
 struct LaneStack {
-    StackT* lds;
+    TPT_LDS StackT* lds;
     int nlds;
     StackT deep[kMaxStackSlots];
     __device__ __forceinline__ void put(int i, int v) {
@@ -397,10 +405,20 @@ __device__ __forceinline__ void light_sample(const DevLight* __restrict__ Ls, in
 
 // sampleEnvLights (:288-294): Vec2UV (env_light.cuh:72-78) + point/clamp fetch
 // (texture.cu:156-170) of the RGBA8 equirect, row 0 = bottom.
-__device__ __noinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
+#ifdef TPT_EXP_ENV_INLINE
+#define TPT_ENV_ATTR __forceinline__
+#else
+#define TPT_ENV_ATTR __noinline__
+#endif
+__device__ TPT_ENV_ATTR V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
+#ifdef TPT_EXP_NO_ENV_TRIG   // timing-only knock-out: wrong texels
+    float u = d.z * 0.5f + 0.5f;
+    const float v = d.y * 0.5f + 0.5f;
+#else
     float u = patan2_fast(d.z, d.x) / (2.0f * kPi);
     if (u < 0.0f) u += 1.0f;
     const float v = 1.0f - pacos_fast(fclamp(d.y, 1.0f, -1.0f)) / kPi;
+#endif
     int ix = (int)floorf(u * (float)w);
     int iy = (int)floorf(v * (float)h);
     ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
@@ -446,7 +464,7 @@ __device__ __forceinline__ uint32_t p_kind(float prob) {
 
 template <int MAXD>
 struct PathRecords {
-    float* lds;                          // this lane's column: word at lds[(level*words + w) * 256]
+    TPT_LDS float* lds;                        // this lane's column: word at lds[(level*words + w) * 256]
     int nlds, words;
     float deep[MAXD * 5];
 
@@ -473,7 +491,7 @@ struct PathRecords {
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
 // state (direct term, normal, light index, incoming direction -- r.d during an
 // extension ray) is dead across traversals and drops out of the registers.
-template <int MAXD, bool ORDERED, bool LIGHTS, typename StackT>
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT>
 __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -485,11 +503,33 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
     const int nint = a.n_faces - 1;
+    // Material table in LDS when small (every shading, probe and unwind step
+    // reads it; LDS latency instead of a dependent global load).  The copy is
+    // the kernel's only barrier.
+    TPT_LDS char* slds = (TPT_LDS char*)lds;
+    TPT_LDS LdsF4* smtl = (TPT_LDS LdsF4*)(slds + a.lds_mtl_offset);
+    if constexpr (MTL_LDS) {
+        for (int i = tid; i < 2 * (a.n_materials + 1); i += 256) {
+            const float4 m = a.mtl[i];
+            smtl[i].x = m.x;
+            smtl[i].y = m.y;
+            smtl[i].z = m.z;
+            smtl[i].w = m.w;
+        }
+        __syncthreads();
+    }
+    auto MT = [&](int i) -> float4 {
+        if constexpr (MTL_LDS) {
+            return make_float4(smtl[i].x, smtl[i].y, smtl[i].z, smtl[i].w);
+        } else {
+            return a.mtl[i];
+        }
+    };
     LaneStack<StackT> stk;
-    stk.lds = (StackT*)lds + tid;
+    stk.lds = (TPT_LDS StackT*)(slds + a.lds_stack_offset) + tid;
     stk.nlds = a.stack_lds_slots;
     PathRecords<MAXD> rec;
-    rec.lds = (float*)(lds + a.lds_rec_offset) + tid;
+    rec.lds = (TPT_LDS float*)(slds + a.lds_rec_offset) + tid;
     rec.nlds = a.rec_lds_levels;
     rec.words = LIGHTS ? 5 : 2;
 
@@ -511,6 +551,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     const int refill = a.refill;
 
 #ifdef TPT_PROFILE_PHASES
+    const unsigned long long t_wave0 = wall_clock64();
     unsigned long long p_done = 0, p_trav = 0, p_steps = 0, t_iter0 = 0, t_loop0 = 0, p_outer = 0;
     unsigned long long p_sub[3] = {0, 0, 0};
 #endif
@@ -540,7 +581,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                                     (r.v * v3(s2.x, s2.y, s2.z)));
                     r.o = r.o + (r.t * rd);
                     const int mtl = __float_as_int(s0.w);
-                    const float4 m1 = a.mtl[2 * mtl + 1];
+                    const float4 m1 = MT(2 * mtl + 1);
                     float af;
                     const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
                     rec.put(depth, 0, af);
@@ -553,7 +594,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 if (r.fid < 0) {   // sampleDeltaLights :279-282 (light re-sampled: deterministic)
                     V3 ldir, lrad;
                     light_sample(a.lights, li, r.o, ldir, lrad);
-                    const float4 m0 = a.mtl[2 * (mk & 0x3fffffffu)];
+                    const float4 m0 = MT(2 * (mk & 0x3fffffffu));
                     direct = direct + (v3(m0.x, m0.y, m0.z) * lrad);
                 }
                 ++li;
@@ -563,7 +604,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 uint32_t pm = kNoProbe;
                 if (r.fid >= 0) {
                     pm = (uint32_t)__float_as_int(a.shade[3 * r.fid].w);
-                    const float e = a.mtl[2 * pm].w;
+                    const float e = MT(2 * pm).w;
                     dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + dl;
                 }
                 rec.put_dst(depth, mk, pm, dl);
@@ -572,7 +613,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             V3 td = rd;
             bool shadow = false;
             if (lights_next) {
-                const float4 m1 = a.mtl[2 * (mk & 0x3fffffffu) + 1];
+                const float4 m1 = MT(2 * (mk & 0x3fffffffu) + 1);
                 if (LIGHTS && li < a.n_lights) {
                     V3 lrad;
                     light_sample(a.lights, li, r.o, td, lrad);
@@ -588,7 +629,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 }
             }
             if (after) {
-                const float e = a.mtl[2 * (mk & 0x3fffffffu)].w;
+                const float e = MT(2 * (mk & 0x3fffffffu)).w;
                 if (e > 0.0f) {   // an emitter ends the path (:408-412); the unwind starts from e
                     L = e * v3(1.0f, 1.0f, 1.0f);
                     finish = true;
@@ -609,7 +650,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     const float af = rec.get(k, 0);
                     const uint32_t w1 = __float_as_uint(rec.get(k, 1));
                     const bool packed = rec.words == 2;
-                    const float4 mb = a.mtl[2 * (w1 & (packed ? 0x7fffu : 0x3fffffffu))];
+                    const float4 mb = MT(2 * (w1 & (packed ? 0x7fffu : 0x3fffffffu)));
                     const V3 att = af * v3(mb.x, mb.y, mb.z);                   // :379
                     const uint32_t kind = w1 >> 30;
                     const float prob = kind == 0u ? af : (kind == 1u ? -0.0f : 0.0f);
@@ -617,7 +658,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     V3 dst;
                     if (packed) {
                         const uint32_t pm = (w1 >> 15) & 0x7fffu;
-                        const float e = pm == kNoProbe ? 0.0f : a.mtl[2 * pm].w;
+                        const float e = pm == kNoProbe ? 0.0f : MT(2 * pm).w;
                         dst = pm == kNoProbe ? v3(0.0f, 0.0f, 0.0f)
                                              : (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + v3(0.0f, 0.0f, 0.0f);
                     } else {
@@ -679,13 +720,14 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         ++p_outer;
 #endif
         // ---- traversal: step while enough lanes of the wave are still traversing ----
+        const int thr = refill;
         for (;;) {
 #ifdef TPT_PROFILE_PHASES
             ++p_steps;
 #endif
             const int cnt = __popcll(__ballot(ts == TS_TRAV));
             if (cnt == 0) break;
-            if (cnt < refill && __ballot(ts == TS_DONE) != 0ull) break;
+            if (cnt < thr && __ballot(ts == TS_DONE) != 0ull) break;
             // Speculative leaf postponement: a lane that reaches a leaf parks it
             // (one slot) and keeps walking inner nodes; the wave runs the
             // triangle branch only when enough lanes hold a parked leaf, when
@@ -751,6 +793,14 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     const unsigned long long s_wide = wave_sum(c_wide);
     const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
                              s_shade = wave_sum(c_shade), s_ovf = wave_sum(c_ovf);
+#ifdef TPT_PROFILE_PHASES
+    unsigned long long m_trav = c_trav;   // heaviest lane's ray count
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o2 = __shfl_xor(m_trav, off, 64);
+        m_trav = o2 > m_trav ? o2 : m_trav;
+    }
+#endif
     if (lane == 0) {
         atomicAdd(&a.counters[0], s_trav);
         atomicAdd(&a.counters[1], s_inner);
@@ -766,6 +816,22 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[10], p_sub[1]);
         atomicAdd(&a.counters[11], p_sub[2]);
         atomicAdd(&a.counters[12], p_outer);
+        const unsigned long long life = wall_clock64() - t_wave0;
+        atomicMax(&a.counters[13], life);
+        atomicAdd(&a.counters[14], life);
+        atomicAdd(&a.counters[15], 1ull);
+        if (a.debug_waves) {   // per-wave record: start, life, steps, shading passes, rays, wide, max lane rays, done-time
+            const unsigned long long wid = ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
+            unsigned long long* o = a.debug_waves + 8 * wid;
+            o[0] = t_wave0;
+            o[1] = life;
+            o[2] = p_steps;
+            o[3] = p_outer;
+            o[4] = s_trav;
+            o[5] = s_wide;
+            o[6] = m_trav;
+            o[7] = p_done;
+        }
 #endif
     }
 }
@@ -815,56 +881,75 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
     }
 }
 
-template <bool ORDERED, bool LIGHTS, typename StackT>
-static void launch_trace_t(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if (a.max_depth <= 8)
-        hipLaunchKernelGGL((k_trace<8, ORDERED, LIGHTS, StackT>), grid, dim3(256), lds, s, a);
-    else
-        hipLaunchKernelGGL((k_trace<64, ORDERED, LIGHTS, StackT>), grid, dim3(256), lds, s, a);
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT>
+static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT>), grid, dim3(256), lds, s, a);
 }
 
-template <bool ORDERED>
-static void launch_trace_o(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
-    const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
-    if (lights) {
-        if (small) launch_trace_t<ORDERED, true, uint16_t>(a, grid, lds, s);
-        else launch_trace_t<ORDERED, true, int>(a, grid, lds, s);
-    } else {
-        if (small) launch_trace_t<ORDERED, false, uint16_t>(a, grid, lds, s);
-        else launch_trace_t<ORDERED, false, int>(a, grid, lds, s);
-    }
+template <bool LIGHTS, bool MTL_LDS, typename StackT>
+static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
+    else launch_one<64, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
 }
 
-// LDS per 256-lane workgroup: the traversal stack, then as many path-record
-// levels as fit in kLdsBudget (TPT_TRACE_WAVES workgroups per CU share the
-// 160 KiB).
+// LDS per 256-lane workgroup: [material table][traversal stack][path records],
+// within kLdsBudget (TPT_TRACE_WAVES workgroups per CU share the 160 KiB).
 constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
+constexpr size_t kLdsMtlMax = 2048;   // material tables up to 64 entries go to LDS
 
-size_t trace_lds_bytes(TraceArgs& a) {
-    const size_t elem = (2 * (size_t)a.n_faces - 1) <= 65535 ? 2 : 4;
+size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds) {
+    const size_t mtl_bytes = (size_t)(a.n_materials + 1) * 2 * sizeof(float4);
+    a.mtl_in_lds = mtl_lds ? 1 : 0;
+    a.lds_mtl_offset = 0;
+    const size_t head = mtl_lds ? (mtl_bytes + 15) / 16 * 16 : 0;
+    const size_t budget = kLdsBudget - head;
     const size_t slot = 256 * elem;
-    const size_t level = (size_t)rec_words(a.n_lights, a.n_materials) * 256 * sizeof(float);
+    const size_t level = (size_t)words * 256 * sizeof(float);
     // Whole stack (capacity + 3 spare slots for the unconditional 4-wide
     // pushes) in LDS when it leaves room for 2 record levels; otherwise the
     // stack's first slots share the budget with 2 levels, the rest is private.
     size_t slots = (size_t)a.stack_depth + 3;
-    if (slots * slot + 2 * level > kLdsBudget) slots = (kLdsBudget - 2 * level) / slot;
+    if (slots * slot + 2 * level > budget) slots = (budget - 2 * level) / slot;
     const size_t stack = (slots * slot + 15) / 16 * 16;
-    size_t levels = stack < kLdsBudget ? (kLdsBudget - stack) / level : 0;
+    size_t levels = stack < budget ? (budget - stack) / level : 0;
     if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;
     a.stack_lds_slots = (int)slots;
-    a.lds_rec_offset = (int)stack;
+    a.lds_stack_offset = (int)head;
+    a.lds_rec_offset = (int)(head + stack);
     a.rec_lds_levels = (int)levels;
-    return stack + levels * level;
+    return head + stack + levels * level;
 }
 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
-    const size_t lds = trace_lds_bytes(a);
     dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
-    if (a.flags & TPT_FLAG_REF_ORDER) launch_trace_o<false>(a, grid, lds, s);
-    else launch_trace_o<true>(a, grid, lds, s);
+    if (a.flags & TPT_FLAG_REF_ORDER) {
+        // the reference's visit order (tests, diagnostics): one general variant
+        const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false);
+        launch_one<64, false, true, false, int>(a, grid, lds, s);
+        return hipGetLastError();
+    }
+    const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
+    const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
+    const bool mtl_lds = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
+    const size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds);
+    if (lights) {
+        if (mtl_lds) {
+            if (small) launch_ordered<true, true, uint16_t>(a, grid, lds, s);
+            else launch_ordered<true, true, int>(a, grid, lds, s);
+        } else {
+            if (small) launch_ordered<true, false, uint16_t>(a, grid, lds, s);
+            else launch_ordered<true, false, int>(a, grid, lds, s);
+        }
+    } else {
+        if (mtl_lds) {
+            if (small) launch_ordered<false, true, uint16_t>(a, grid, lds, s);
+            else launch_ordered<false, true, int>(a, grid, lds, s);
+        } else {
+            if (small) launch_ordered<false, false, uint16_t>(a, grid, lds, s);
+            else launch_ordered<false, false, int>(a, grid, lds, s);
+        }
+    }
     return hipGetLastError();
 }
 
