@@ -6,10 +6,11 @@
 //       q2 = (R.min.z, R.max.xyz)  q3 = (bits(left), bits(right), 0, 0)
 //     child ids use the reference numbering (bvh.cu:164-214): id >= F-1 is
 //     the leaf at sorted position id-(F-1).
-//   inner4[8*(F-1)] float4  4-wide view for the ordered traversal: slot i is
-//     filled for internal node i at even depth and holds its up to 4
-//     grandchildren (a leaf child stands for itself): child k box = floats
-//     6k..6k+5 of q0..q5 (min.xyz, max.xyz), q6 = child ids (-1: none).
+//   inner4[8*n4] float4  4-wide view for the ordered traversal: one node per
+//     even-depth internal node, numbered breadth-first (root 0), holding its up
+//     to 4 grandchildren (a leaf child stands for itself): child k box = floats
+//     6k..6k+5 of q0..q5 (min.xyz, max.xyz), q6 = child ids (-1: none; a 4-wide
+//     node id < F-1, or F-1 + leaf position).
 //   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
 //   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, 0), (n2.xyz, 0)
 //   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)
@@ -38,6 +39,9 @@ struct TraceArgs {
     // scene
     const float4* inner;
     const float4* inner4;
+    int32_t n4;                          // 4-wide nodes
+    int32_t lds_nodes;                   // set by launch_trace: 4-wide nodes [0, lds_nodes) staged in LDS
+    int32_t lds_nodes_offset;            // set by launch_trace: their byte offset in LDS
     const float4* tri;
     const float4* shade;
     const float4* mtl;
@@ -121,7 +125,12 @@ struct BuildBuffers {
     uint32_t* parent;                    // 2F-1
     float* node_box;                     // 6 per node (2F-1)
     uint32_t* flags;                     // F-1
-    uint32_t* max_depth;                 // 2: deepest leaf, non-finite inner-box flag
+    uint32_t* max_depth;                 // 3: deepest leaf, non-finite inner-box flag, 4-wide node count
+    unsigned long long* bfs_keys;        // F-1: (level, id) keys of the 4-wide nodes
+    unsigned long long* bfs_keys_sorted;
+    uint32_t* bfs_ids;                   // F-1
+    uint32_t* bfs_ids_sorted;
+    uint32_t* bfs_newid;                 // F-1: binary id -> breadth-first 4-wide id
     void* sort_tmp;
     size_t sort_tmp_bytes;
     // outputs
@@ -132,6 +141,7 @@ struct BuildBuffers {
     void* nodes36;                       // reference layout (2F-1) * 36 B
     uint32_t out_max_depth;              // deepest leaf (root = 0), set by launch_build
     uint32_t out_boxes_finite;           // 1: every inner-node child box is finite
+    uint32_t out_n4;                     // 4-wide nodes (breadth-first prefix of inner4)
 };
 hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes);
 hipError_t launch_build(BuildBuffers& b, hipStream_t s);

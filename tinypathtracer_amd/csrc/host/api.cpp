@@ -121,6 +121,7 @@ struct tpt_scene {
     bool built = false;
     int32_t stack_depth = 0;
     int32_t boxes_finite = 0;
+    int32_t n4 = 0;
     uint32_t tree_depth = 0;
     // inputs
     DevBuf<uint32_t> indices;
@@ -131,8 +132,8 @@ struct tpt_scene {
     DevBuf<uint32_t> jumps;
     // world + BVH
     DevBuf<float> wverts, wnorms, leaf_box, node_box;
-    DevBuf<unsigned long long> keys, keys_sorted;
-    DevBuf<uint32_t> fids, fids_sorted, parent, flags, max_depth;
+    DevBuf<unsigned long long> keys, keys_sorted, bfs_keys, bfs_keys_sorted;
+    DevBuf<uint32_t> fids, fids_sorted, parent, flags, max_depth, bfs_ids, bfs_ids_sorted, bfs_newid;
     DevBuf<int2> children;
     DevBuf<uint8_t> sort_tmp, nodes36;
     DevBuf<float4> inner, inner4, tri, shade;
@@ -259,7 +260,12 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     HIP_OR_FAIL(s->parent.alloc(nn));
     HIP_OR_FAIL(s->node_box.alloc(6 * nn));
     HIP_OR_FAIL(s->flags.alloc(nn));
-    HIP_OR_FAIL(s->max_depth.alloc(2));
+    HIP_OR_FAIL(s->max_depth.alloc(3));
+    HIP_OR_FAIL(s->bfs_keys.alloc(std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->bfs_keys_sorted.alloc(std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->bfs_ids.alloc(std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->bfs_ids_sorted.alloc(std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->bfs_newid.alloc(std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->sort_tmp.alloc(std::max<size_t>(sort_bytes, 16)));
     HIP_OR_FAIL(s->inner.alloc(4 * std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->inner4.alloc(8 * std::max<size_t>(n - 1, 1)));
@@ -296,12 +302,18 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     b.sort_tmp_bytes = sort_bytes;
     b.inner = s->inner.p;
     b.inner4 = s->inner4.p;
+    b.bfs_keys = s->bfs_keys.p;
+    b.bfs_keys_sorted = s->bfs_keys_sorted.p;
+    b.bfs_ids = s->bfs_ids.p;
+    b.bfs_ids_sorted = s->bfs_ids_sorted.p;
+    b.bfs_newid = s->bfs_newid.p;
     b.tri = s->tri.p;
     b.shade = s->shade.p;
     b.nodes36 = s->nodes36.p;
     HIP_OR_FAIL(tpt::launch_build(b, s->stream));
     s->tree_depth = b.out_max_depth;
     s->boxes_finite = (int32_t)b.out_boxes_finite;
+    s->n4 = (int32_t)b.out_n4;
     // Stack capacity: the binary DFS that pushes one sibling per level holds at
     // most depth + 1 entries; the 4-wide ordered traversal pushes up to 3 per
     // 4-wide node, one per two levels: 3 * ceil(depth / 2).
@@ -345,6 +357,7 @@ void tpt_env_destroy(tpt_env* env) {
 static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, tpt::TraceArgs& a) {
     a.inner = s->inner.p;
     a.inner4 = s->inner4.p;
+    a.n4 = s->n4;
     a.tri = s->tri.p;
     a.shade = s->shade.p;
     a.mtl = s->mtl.p;

@@ -198,8 +198,25 @@ __global__ void k_pack_inner(BuildBuffers b) {
     if (!fin) atomicOr(b.max_depth + 1, 1u);
 }
 
-// 4-wide nodes for even-depth internal nodes: the children of a kept node's
-// internal children are themselves kept (depth + 2), so depth parity decides.
+// 4-wide nodes are the even-depth internal nodes: the children of a kept
+// node's internal children are themselves kept (depth + 2), so depth parity
+// decides.  They are numbered breadth-first -- key (level, id), odd-depth nodes
+// sorted past the end -- so the top levels are a prefix the trace kernel can
+// stage in LDS.
+__global__ void k_bfs_keys(BuildBuffers b, const uint32_t* __restrict__ depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= b.n_faces - 1) return;
+    const uint32_t d = depth[i];
+    b.bfs_keys[i] = (d & 1u) ? ~0ull : (((unsigned long long)(d >> 1) << 32) | (unsigned)i);
+    b.bfs_ids[i] = (uint32_t)i;
+    if (!(d & 1u)) atomicAdd(b.max_depth + 2, 1u);
+}
+
+__global__ void k_bfs_newid(BuildBuffers b, uint32_t n4) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n4) b.bfs_newid[b.bfs_ids_sorted[j]] = j;
+}
+
 __global__ void k_pack_inner4(BuildBuffers b, const uint32_t* __restrict__ depth) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int nint = b.n_faces - 1;
@@ -225,11 +242,15 @@ __global__ void k_pack_inner4(BuildBuffers b, const uint32_t* __restrict__ depth
 #pragma unroll
         for (int j = 0; j < 6; ++j) f[6 * k + j] = ids[k] < 0 ? 0.0f : bx[j];
     }
-    float4* q = b.inner4 + 8 * i;
+    float4* q = b.inner4 + 8 * (size_t)b.bfs_newid[i];
 #pragma unroll
     for (int k = 0; k < 6; ++k) q[k] = make_float4(f[4 * k], f[4 * k + 1], f[4 * k + 2], f[4 * k + 3]);
-    q[6] = make_float4(__int_as_float(ids[0]), __int_as_float(ids[1]), __int_as_float(ids[2]),
-                       __int_as_float(ids[3]));
+    int out[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)   // internal grandchildren -> breadth-first id; leaves keep nint + position
+        out[k] = (ids[k] >= 0 && ids[k] < nint) ? (int)b.bfs_newid[ids[k]] : ids[k];
+    q[6] = make_float4(__int_as_float(out[0]), __int_as_float(out[1]), __int_as_float(out[2]),
+                       __int_as_float(out[3]));
     q[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
@@ -283,10 +304,16 @@ __global__ void k_pack_nodes36(BuildBuffers b) {
 }
 
 hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes) {
-    *bytes = 0;
-    return rocprim::radix_sort_pairs((void*)nullptr, *bytes, (unsigned long long*)nullptr,
-                                     (unsigned long long*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                     (size_t)n, 0, 63);
+    // the Morton sort (63 bits) and the breadth-first numbering sort (64 bits) share the buffer
+    size_t a = 0, b = 0;
+    hipError_t e = rocprim::radix_sort_pairs((void*)nullptr, a, (unsigned long long*)nullptr,
+                                             (unsigned long long*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                             (size_t)n, 0, 63);
+    if (e != hipSuccess) return e;
+    e = rocprim::radix_sort_pairs((void*)nullptr, b, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                  (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 64);
+    *bytes = a > b ? a : b;
+    return e;
 }
 
 #define TPT_TRY(x)                         \
@@ -312,7 +339,8 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s) {
         TPT_TRY(hipGetLastError());
     }
     uint32_t* depth = b.flags;   // reused: 2F-1 words
-    TPT_TRY(hipMemsetAsync(b.max_depth, 0, 2 * sizeof(uint32_t), s));
+    TPT_TRY(hipMemsetAsync(b.max_depth, 0, 3 * sizeof(uint32_t), s));
+    b.out_n4 = 0;
     hipLaunchKernelGGL(k_depth, grid(nn), blk, 0, s, b, depth);
     TPT_TRY(hipGetLastError());
     uint32_t maxd = 0;
@@ -326,6 +354,17 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s) {
     }
     if (n > 1) {
         hipLaunchKernelGGL(k_pack_inner, grid(n - 1), blk, 0, s, b);
+        TPT_TRY(hipGetLastError());
+        hipLaunchKernelGGL(k_bfs_keys, grid(n - 1), blk, 0, s, b, depth);
+        TPT_TRY(hipGetLastError());
+        size_t tmp2 = b.sort_tmp_bytes;
+        TPT_TRY(rocprim::radix_sort_pairs(b.sort_tmp, tmp2, b.bfs_keys, b.bfs_keys_sorted, b.bfs_ids,
+                                          b.bfs_ids_sorted, (size_t)(n - 1), 0, 64, s));
+        uint32_t n4 = 0;
+        TPT_TRY(hipMemcpyAsync(&n4, b.max_depth + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        TPT_TRY(hipStreamSynchronize(s));
+        b.out_n4 = n4;
+        hipLaunchKernelGGL(k_bfs_newid, grid((int)n4), blk, 0, s, b, n4);
         TPT_TRY(hipGetLastError());
         hipLaunchKernelGGL(k_pack_inner4, grid(n - 1), blk, 0, s, b, depth);
         TPT_TRY(hipGetLastError());

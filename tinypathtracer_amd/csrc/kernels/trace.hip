@@ -20,6 +20,8 @@
 //    loads), triangles are pre-gathered (v0, e1, e2, fid: three 16-B loads).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../common/device_api.hpp"
 #include "../common/ptrig.hpp"
 #include "../common/rng.hpp"
@@ -31,6 +33,13 @@
 #endif
 #ifndef TPT_LEAF_KP
 #define TPT_LEAF_KP 24    // ... or this many lanes hold a parked leaf
+#endif
+// Top 4-wide nodes staged in LDS (breadth-first prefix of inner4).  Off by
+// default: measured on box 256 spp, 14 staged nodes cost 10 % (the per-visit
+// LDS/global branch and LDS reads outweigh the shorter latency of the first
+// levels); build with -DTPT_LDS_NODES_MAX=4096 to stage up to 32.
+#ifndef TPT_LDS_NODES_MAX
+#define TPT_LDS_NODES_MAX 0
 #endif
 #ifndef TPT_TRACE_WAVES
 #define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator
@@ -205,11 +214,35 @@ struct LaneStack {
 // is the binary traversal's.  Hit children are sorted by slab entry; the
 // nearest is returned, the others (up to 3) are pushed farthest-first.  The
 // stack region has 3 spare slots so all three writes are unconditional.
+__device__ __forceinline__ float4 lds_f4(const TPT_LDS LdsF4* p) { return make_float4(p->x, p->y, p->z, p->w); }
+
+// (packed v_pk_add/v_pk_mul slab math was measured 17 % slower: register-pair
+// constraints outweigh the halved instruction count)
+
 template <typename StackT>
-__device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4, LaneStack<StackT>& stk,
+__device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4,
+                                            const TPT_LDS LdsF4* snodes, int nlds_nodes, LaneStack<StackT>& stk,
                                             int& sp) {
-    const float4* nd = inner4 + 8 * r.node;
-    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
+    float4 q0, q1, q2, q3, q4, q5, q6;
+    if (TPT_LDS_NODES_MAX > 0 && r.node < nlds_nodes) {   // top levels, staged in LDS at kernel start
+        const TPT_LDS LdsF4* nd = snodes + 8 * r.node;
+        q0 = lds_f4(nd);
+        q1 = lds_f4(nd + 1);
+        q2 = lds_f4(nd + 2);
+        q3 = lds_f4(nd + 3);
+        q4 = lds_f4(nd + 4);
+        q5 = lds_f4(nd + 5);
+        q6 = lds_f4(nd + 6);
+    } else {
+        const float4* nd = inner4 + 8 * r.node;
+        q0 = nd[0];
+        q1 = nd[1];
+        q2 = nd[2];
+        q3 = nd[3];
+        q4 = nd[4];
+        q5 = nd[5];
+        q6 = nd[6];
+    }
     float k0, k1, k2, k3, e0, e1, e2, e3;
     slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
@@ -516,8 +549,18 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             smtl[i].z = m.z;
             smtl[i].w = m.w;
         }
-        __syncthreads();
     }
+    // the top 4-wide nodes (breadth-first prefix of inner4): every ray starts
+    // there, so their loads become LDS reads
+    TPT_LDS LdsF4* snodes = (TPT_LDS LdsF4*)(slds + a.lds_nodes_offset);
+    for (int i = tid; i < 8 * a.lds_nodes; i += 256) {
+        const float4 m = a.inner4[i];
+        snodes[i].x = m.x;
+        snodes[i].y = m.y;
+        snodes[i].z = m.z;
+        snodes[i].w = m.w;
+    }
+    if (MTL_LDS || a.lds_nodes > 0) __syncthreads();
     auto MT = [&](int i) -> float4 {
         if constexpr (MTL_LDS) {
             return make_float4(smtl[i].x, smtl[i].y, smtl[i].z, smtl[i].w);
@@ -743,7 +786,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     int next;
                     if (ORDERED && r.fin) {   // 4-wide (r.fin includes a.boxes_finite)
                         ++c_wide;
-                        next = inner_visit4(r, a.inner4, stk, r.sp);
+                        next = inner_visit4(r, a.inner4, snodes, a.lds_nodes, stk, r.sp);
                     } else {                  // binary, the reference's exact slab test
                         ++c_inner;
                         int deferred;
@@ -895,24 +938,33 @@ static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_
 // LDS per 256-lane workgroup: [material table][traversal stack][path records],
 // within kLdsBudget (TPT_TRACE_WAVES workgroups per CU share the 160 KiB).
 constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
-constexpr size_t kLdsMtlMax = 2048;   // material tables up to 64 entries go to LDS
+constexpr size_t kLdsMtlMax = 2048;    // material tables up to 64 entries go to LDS
+constexpr size_t kLdsNodesMax = TPT_LDS_NODES_MAX;
 
-size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds) {
-    const size_t mtl_bytes = (size_t)(a.n_materials + 1) * 2 * sizeof(float4);
+size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide) {
+    // [material table][top 4-wide nodes][traversal stack][path records].
+    // Priorities (measured on box): the whole stack (a
+    // stack capped at 23 of its 40 slots cost 7 %), then path records up to
+    // max_depth (records of long paths in private memory slow the heaviest
+    // tiles), then as many top nodes as the remaining bytes hold.
+    const size_t mtl_bytes = mtl_lds ? ((size_t)(a.n_materials + 1) * 2 * 16 + 127) / 128 * 128 : 0;
     a.mtl_in_lds = mtl_lds ? 1 : 0;
     a.lds_mtl_offset = 0;
-    const size_t head = mtl_lds ? (mtl_bytes + 15) / 16 * 16 : 0;
-    const size_t budget = kLdsBudget - head;
+    const size_t budget = kLdsBudget - mtl_bytes;
     const size_t slot = 256 * elem;
     const size_t level = (size_t)words * 256 * sizeof(float);
-    // Whole stack (capacity + 3 spare slots for the unconditional 4-wide
-    // pushes) in LDS when it leaves room for 2 record levels; otherwise the
-    // stack's first slots share the budget with 2 levels, the rest is private.
+    // whole stack (capacity + 3 spare slots for the unconditional 4-wide
+    // pushes) when 2 record levels still fit; else its first slots, the rest private
     size_t slots = (size_t)a.stack_depth + 3;
     if (slots * slot + 2 * level > budget) slots = (budget - 2 * level) / slot;
     const size_t stack = (slots * slot + 15) / 16 * 16;
-    size_t levels = stack < budget ? (budget - stack) / level : 0;
+    size_t levels = (budget - stack) / level;
     if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;
+    size_t nodes = wide ? (budget - stack - levels * level) / 128 : 0;
+    nodes = std::min(nodes, std::min<size_t>((size_t)a.n4, kLdsNodesMax / 128));
+    a.lds_nodes = (int)nodes;
+    a.lds_nodes_offset = (int)mtl_bytes;
+    const size_t head = mtl_bytes + nodes * 128;
     a.stack_lds_slots = (int)slots;
     a.lds_stack_offset = (int)head;
     a.lds_rec_offset = (int)(head + stack);
@@ -925,14 +977,14 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
     if (a.flags & TPT_FLAG_REF_ORDER) {
         // the reference's visit order (tests, diagnostics): one general variant
-        const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false);
+        const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, false);
         launch_one<64, false, true, false, int>(a, grid, lds, s);
         return hipGetLastError();
     }
     const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
     const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
     const bool mtl_lds = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
-    const size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds);
+    const size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true);
     if (lights) {
         if (mtl_lds) {
             if (small) launch_ordered<true, true, uint16_t>(a, grid, lds, s);
