@@ -104,19 +104,34 @@ def data_note(args):
 
 
 def cpu_baseline(args):
-    """The oracle (CPU port of the reference kernels) on the host cores, same
-    scene/resolution/depth, bounded spp; trace phase only (RNG init reported
-    separately, like the reference's per-frame curand_init)."""
+    """The oracle (CPU port of the reference kernels) on the host cores: the
+    bench workload at a bounded spp (Mrays/s does not depend on spp), plus
+    SURVEY 8(d) C1 (box 256x256, 16 spp, depth 4).  Trace phase only (RNG init
+    reported separately, like the reference's per-frame curand_init); best of
+    3 runs each."""
     from oracle import oracle as O
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+
+    def best_of(ps, w, h, spp, depth, n=3):
+        best = None
+        for _ in range(n):
+            _, _, c = O.render(ps, w, h, spp, depth, args.seed, trig_mode=1, threads=threads)
+            if best is None or c["trace_ms"] < best["trace_ms"]:
+                best = c
+        return best
+
     ps = O.load_scene(scene_file(args.scene))
-    _, _, c = O.render(ps, args.width, args.height, args.cpu_spp, args.depth, args.seed, trig_mode=1,
-                       threads=threads)
+    c = best_of(ps, args.width, args.height, args.cpu_spp, args.depth)
     mrays = c["traversals"] / (c["trace_ms"] * 1e3)
+    c1 = best_of(O.load_scene(scene_file("box")), 256, 256, 16, 4)
+    c1_mrays = c1["traversals"] / (c1["trace_ms"] * 1e3)
     return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{args.scene}.gltf {args.width}x{args.height} x {args.cpu_spp} spp, depth {args.depth}, "
-                      f"seed {args.seed}: {c['traversals']} rays in {c['trace_ms'] / 1e3:.2f} s trace "
+                      f"seed {args.seed}, best of 3: {c['traversals']} rays in {c['trace_ms'] / 1e3:.2f} s trace "
                       f"(+{c['init_ms'] / 1e3:.2f} s RNG init not counted)",
+            "c1": {"value": round(c1_mrays, 3), "unit": "Mrays/s",
+                   "sample": f"box.gltf 256x256 x 16 spp, depth 4, seed {args.seed}, best of 3: "
+                             f"{c1['traversals']} rays in {c1['trace_ms'] / 1e3:.3f} s trace"},
             "cpu_model": _cpu_model()}
 
 
