@@ -43,6 +43,10 @@ def parse():
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="SURVEY 8(d) preset; explicit flags after it still override")
     ap.add_argument("--scene", default="box")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="gloo: rehearse the N-rank path on one GPU (all ranks on device 0, gather via host)")
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="rank 0 re-renders the whole frame alone and checks the gathered frame bit for bit")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of an N-rank run: render only rank 0's bands of an N-way split")
     ap.add_argument("--env", choices=["sky", "none"], default=None, help="procedural equirect env on miss")
@@ -157,11 +161,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = local
+    # one process per GPU; the gloo rehearsal maps every rank onto the visible devices
+    dev = local if args.dist_backend == "nccl" else local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     scene = T.Scene(scene_file(args.scene))
     d_scene = scene.copySceneToDevice(dev)
@@ -183,8 +190,10 @@ def main():
         st = pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,
                         radiance=radiance, band=band, spp_per_launch=args.spp_per_launch,
                         flags=args.flags, refill=args.refill)
-        frame = shard.gather_frame(radiance, H, args.band_rows, world, rank) if world > 1 else radiance
-        return st, frame
+        if world == 1:
+            return st, radiance
+        src = radiance if args.dist_backend == "nccl" else radiance.cpu()   # gloo gathers host tensors
+        return st, shard.gather_frame(src, H, args.band_rows, world, rank)
 
     for _ in range(args.warmup):
         step()
@@ -206,7 +215,8 @@ def main():
     keys = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
             "rng_init_ms", "resolve_ms", "trace_launches"]
     local_tot = {k: float(sum(s[k] for s in stats)) for k in keys}
-    vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64, device=f"cuda:{dev}")
+    vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64,
+                       device=f"cuda:{dev}" if args.dist_backend == "nccl" else "cpu")
     if world > 1:
         mx = vec.clone()
         dist.all_reduce(vec, op=dist.ReduceOp.SUM)
@@ -237,7 +247,8 @@ def main():
                               + (" env sky" if args.env else ""),
                   "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
                   "max_depth": args.depth, "seed": args.seed,
-                  "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + RCCL gather"
+                  "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + "
+                                 + ("RCCL gather" if args.dist_backend == "nccl" else "gloo gather (1-GPU rehearsal)")
                   if world > 1 else "1 GPU"}
         if os.path.exists(args.pmc_json):
             try:
@@ -276,6 +287,14 @@ def main():
                                    "resolve": round(l_tot["resolve_ms"] / K, 3),
                                    "bvh_build_once": round(build_ms, 3)},
         }
+        if world > 1 and args.verify_gather:
+            # the assembled frame must equal one GPU rendering every row (the RNG
+            # subsequence is the global pixel index, path_tracer.cu:39,320)
+            full = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
+            pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,
+                       radiance=full, band=(args.band_rows, 1, 0), refill=args.refill)
+            got = frame.to(full.device).contiguous()
+            out["gather_verified"] = bool(torch.equal(got.view(torch.int32), full.view(torch.int32)))
         if world == 1 and args.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
