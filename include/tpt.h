@@ -97,6 +97,9 @@ typedef struct {
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
 #define TPT_FLAG_REF_ORDER     0x2   /* reference right-first traversal, no culling */
+#define TPT_FLAG_ACCUMULATE    0x4   /* progressive: continue the previous call's per-pixel streams and
+                                        sums (same frame size, bands and seed); the output is the mean over
+                                        all accumulated samples, bit-identical to one call with their total */
 
 typedef struct {
     uint64_t traversals;          /* traverseBVH calls: primary+extension+probe+shadow */
@@ -112,6 +115,7 @@ typedef struct {
     int32_t trace_launches;
     int32_t pad;
     uint64_t wide_visits;         /* 4-wide internal nodes popped (ordered traversal) */
+    uint64_t accumulated_spp;     /* samples per pixel in the output (> spp with TPT_FLAG_ACCUMULATE) */
 } tpt_stats;
 
 typedef struct tpt_scene tpt_scene;

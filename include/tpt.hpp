@@ -150,28 +150,34 @@ public:
 
     // doTrace (path_tracer.cu:491-554): one frame into a caller framebuffer
     // (host or device pointer, W*H*4 BGRA).  seed 0 -> time(), as the reference.
+    // accumulate: progressive rendering (TPT_FLAG_ACCUMULATE) -- continue the
+    // previous call's samples for the same frame instead of starting afresh
+    // (the reference re-renders fresh samples every frame, vkEngine.cu:244).
     tpt_stats doTrace(DeviceScene& scene, const Camera& camera, uint8_t* framebuffer, int nSamplesPerPixel,
                       uint64_t seed = 0, int max_depth = 8, float* radiance = nullptr,
-                      int band_count = 1, int band_index = 0) {
+                      int band_count = 1, int band_index = 0, bool accumulate = false) {
         if (!scene.built()) scene.build();
         tpt_params p{};
         p.width = m_width;
         p.height = m_height;
         p.spp = nSamplesPerPixel;
         p.max_depth = max_depth;
-        p.seed = seed ? seed : (uint64_t)std::time(nullptr);
+        p.seed = seed ? seed : (accumulate && last_seed_ ? last_seed_ : (uint64_t)std::time(nullptr));
+        last_seed_ = p.seed;
         p.band_rows = 16;
         p.band_count = band_count;
         p.band_index = band_index;
+        p.flags = accumulate ? TPT_FLAG_ACCUMULATE : 0;
         tpt_stats st{};
         check(tpt_render(scene.handle(), envLight.handle(), &camera.c, &p, radiance, framebuffer, &st));
         return st;
     }
 
     // render(meshFile) (path_tracer.cu:556-579), headless: the reference loops
-    // frames in a window; this renders `frames` frames and returns the last.
+    // frames in a window; this renders `frames` frames and returns the last --
+    // with progressive = true each frame adds its samples to the previous ones.
     Frame render(const std::string& meshFile, int nSamplesPerPixel = 64, uint64_t seed = 0, int max_depth = 8,
-                 int frames = 1) {
+                 int frames = 1, bool progressive = false) {
         Scene scene(meshFile, "gltf");
         DeviceScene d = scene.copySceneToDevice(device_);
         d.build();
@@ -181,7 +187,8 @@ public:
         f.bgra.assign((size_t)m_width * m_height * 4, 255);
         f.radiance.assign((size_t)m_width * m_height * 3, 0.0f);
         for (int i = 0; i < frames; ++i)
-            f.stats = doTrace(d, scene.m_camera, f.bgra.data(), nSamplesPerPixel, seed, max_depth, f.radiance.data());
+            f.stats = doTrace(d, scene.m_camera, f.bgra.data(), nSamplesPerPixel, seed, max_depth, f.radiance.data(),
+                              1, 0, progressive && i > 0);
         return f;
     }
 
@@ -189,6 +196,7 @@ public:
 
 private:
     int device_;
+    uint64_t last_seed_ = 0;
     EnvLight envLight;
 };
 

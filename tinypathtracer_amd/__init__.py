@@ -283,14 +283,22 @@ class PathTracer:
 
     def doTrace(self, d_scene: DeviceScene, camera: Camera, framebuffer=None, nSamplesPerPixel: int = 64,
                 seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
-                flags: int = 0, refill: int = 0):
+                flags: int = 0, refill: int = 0, accumulate: bool = False):
         """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
-        or torch CUDA tensors / raw device pointers (device, int)."""
+        or torch CUDA tensors / raw device pointers (device, int).
+        accumulate=True: progressive rendering (TPT_FLAG_ACCUMULATE) -- continue
+        the previous call's samples of the same frame; with seed None the
+        previous seed is kept (the reference re-seeds from time() every frame)."""
         if not d_scene.built:
             d_scene.build()
         W, H = self.m_width, self.m_height
+        if accumulate:
+            flags |= _lib.FLAG_ACCUMULATE
+            if seed is None:
+                seed = getattr(self, "_last_seed", None)
         if seed is None:
             seed = int(time.time())
+        self._last_seed = seed
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags,
                         refill)
         st = _lib.Stats()

@@ -16,6 +16,7 @@ TPT_OK = 0
 STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "HIP_ERROR", 3: "OOM", 4: "IO", 5: "PARSE", 6: "NO_DEVICE"}
 FLAG_NO_COUNTERS = 0x1
 FLAG_REF_ORDER = 0x2
+FLAG_ACCUMULATE = 0x4
 
 
 class Material(C.Structure):
@@ -61,7 +62,7 @@ class Stats(C.Structure):
                 ("shade_hits", C.c_uint64), ("pixels", C.c_uint64), ("samples", C.c_uint64),
                 ("rng_init_ms", C.c_double), ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("total_ms", C.c_double), ("trace_launches", C.c_int32), ("pad", C.c_int32),
-                ("wide_visits", C.c_uint64)]
+                ("wide_visits", C.c_uint64), ("accumulated_spp", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}

@@ -143,6 +143,10 @@ struct tpt_scene {
     DevBuf<uint8_t> bgra_tmp;
     DevBuf<unsigned long long> counters, debug;
     size_t frame_pixels = 0;
+    // progressive accumulation (TPT_FLAG_ACCUMULATE): the frame the rng/accum state belongs to
+    bool acc_valid = false;
+    int acc_w = 0, acc_h = 0, acc_rows = 0, acc_count = 0, acc_index = 0;
+    uint64_t acc_seed = 0, acc_spp = 0;
 
     ~tpt_scene() {
         DeviceGuard g(device);
@@ -404,18 +408,24 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     const size_t npix = (size_t)W * (size_t)H;
     const int bh = band_height_of(H, band_rows, band_count, p->band_index);
 
+    const bool resume = (p->flags & TPT_FLAG_ACCUMULATE) && s->acc_valid && s->acc_w == W && s->acc_h == H &&
+                        s->acc_rows == band_rows && s->acc_count == band_count && s->acc_index == p->band_index &&
+                        s->acc_seed == p->seed && s->rng.n == 6 * npix && s->accum.n == 3 * npix;
+    s->acc_valid = false;   // re-armed once this call has completed
     HIP_OR_FAIL(s->rng.alloc(6 * npix));
     HIP_OR_FAIL(s->accum.alloc(3 * npix));
     HIP_OR_FAIL(s->counters.alloc(16));
-    HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * sizeof(float), st));   // thrust::fill (:534)
+    if (!resume) HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * sizeof(float), st));   // thrust::fill (:534)
     HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 16 * sizeof(unsigned long long), st));
 
-    // setupRandSeed (:513)
+    // setupRandSeed (:513); a progressive call continues the persisted streams
     HIP_OR_FAIL(hipEventRecord(s->ev[0], st));
-    if (bh > 0)
+    if (bh > 0 && !resume)
         HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, p->seed, W, band_rows, band_count, p->band_index, bh, H,
                                          s->rng.p, st));
     HIP_OR_FAIL(hipEventRecord(s->ev[1], st));
+    const uint64_t total_spp = (resume ? s->acc_spp : 0) + (uint64_t)p->spp;
+    if (total_spp > (uint64_t)INT32_MAX) return fail(TPT_ERR_INVALID_ARG, "accumulated spp overflow");
 
     tpt::TraceArgs a{};
     fill_trace_args(s, env, cam, a);
@@ -476,7 +486,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     r.band_count = band_count;
     r.band_index = p->band_index;
     r.band_height = bh;
-    r.spp = p->spp;
+    r.spp = (int)total_spp;
     if (radiance_out) {
         if (rad_dev) {
             r.radiance = radiance_out;
@@ -526,6 +536,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
         stats->traversals = cnt[0];
         stats->internal_visits = cnt[1];
         stats->wide_visits = cnt[5];
+        stats->accumulated_spp = total_spp;
         stats->leaf_tests = cnt[2];
         stats->shade_hits = cnt[3];
         stats->pixels = (uint64_t)W * (uint64_t)bh;
@@ -540,6 +551,16 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
         stats->total_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
+    // the persisted streams and sums now belong to this frame: a following
+    // TPT_FLAG_ACCUMULATE call with the same frame continues them
+    s->acc_valid = true;
+    s->acc_w = W;
+    s->acc_h = H;
+    s->acc_rows = band_rows;
+    s->acc_count = band_count;
+    s->acc_index = p->band_index;
+    s->acc_seed = p->seed;
+    s->acc_spp = total_spp;
     return TPT_OK;
 }
 

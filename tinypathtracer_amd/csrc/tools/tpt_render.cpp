@@ -5,6 +5,7 @@
 //
 //   tpt_render scene.gltf [--width W] [--height H] [--spp N] [--depth D]
 //              [--seed S] [--env equirect.ppm|--sky] [--out prefix] [--device i]
+//              [--frames F [--progressive]]
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -66,11 +67,12 @@ std::vector<uint8_t> procedural_sky(int w, int h) {
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s scene.gltf [--width W] [--height H] [--spp N] [--depth D] [--seed S] "
-                             "[--env file.ppm | --sky] [--out prefix] [--device i]\n", argv[0]);
+                             "[--env file.ppm | --sky] [--out prefix] [--device i] [--frames F [--progressive]]\n", argv[0]);
         return 2;
     }
     std::string scene_file = argv[1], env_file, out = "out";
-    int W = 1920, H = 1080, spp = 64, depth = 8, device = 0;
+    int W = 1920, H = 1080, spp = 64, depth = 8, device = 0, frames = 1;
+    bool progressive = false;
     uint64_t seed = 0;
     bool sky = false;
     for (int i = 2; i < argc; ++i) {
@@ -88,6 +90,8 @@ int main(int argc, char** argv) {
         else if (a == "--sky") sky = true;
         else if (a == "--out") out = next();
         else if (a == "--device") device = std::stoi(next());
+        else if (a == "--frames") frames = std::stoi(next());
+        else if (a == "--progressive") progressive = true;
         else { std::fprintf(stderr, "unknown option %s\n", a.c_str()); return 2; }
     }
     try {
@@ -102,7 +106,7 @@ int main(int argc, char** argv) {
             env = tpt::EnvLight(img.data(), 2048, 1024, device);
         }
         tpt::PathTracer pt(env, W, H, device);
-        tpt::Frame f = pt.render(scene_file, spp, seed, depth);
+        tpt::Frame f = pt.render(scene_file, spp, seed, depth, frames, progressive);
         std::ofstream ppm(out + ".ppm", std::ios::binary);
         ppm << "P6\n" << W << " " << H << "\n255\n";
         for (size_t i = 0; i < (size_t)W * H; ++i) {   // BGRA -> RGB, rows already top-down
@@ -113,9 +117,10 @@ int main(int argc, char** argv) {
         pfm << "PF\n" << W << " " << H << "\n-1.0\n";
         pfm.write((const char*)f.radiance.data(), (std::streamsize)(f.radiance.size() * sizeof(float)));
         const tpt_stats& s = f.stats;
-        std::printf("{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"spp\": %d, \"rays\": %llu, "
+        std::printf("{\"scene\": \"%s\", \"width\": %d, \"height\": %d, \"spp\": %llu, \"rays\": %llu, "
                     "\"trace_ms\": %.3f, \"mrays_per_s\": %.1f, \"out\": \"%s.ppm\"}\n",
-                    scene_file.c_str(), W, H, spp, (unsigned long long)s.traversals, s.trace_ms,
+                    scene_file.c_str(), W, H, (unsigned long long)s.accumulated_spp, (unsigned long long)s.traversals,
+                    s.trace_ms,
                     s.trace_ms > 0 ? s.traversals / (s.trace_ms * 1e3) : 0.0, out.c_str());
     } catch (const std::exception& e) {
         std::cerr << e.what() << std::endl;   // render() prints and returns (path_tracer.cu:575-578)
