@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of an N-rank run: render only rank 0's bands of an N-way split")
     ap.add_argument("--env", choices=["sky", "none"], default=None, help="procedural equirect env on miss")
+    ap.add_argument("--env-is", action="store_true",
+                    help="opt-in env next-event estimation with importance sampling (A15; changes the image)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=1024)
@@ -189,7 +191,7 @@ def main():
     def step():
         st = pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,
                         radiance=radiance, band=band, spp_per_launch=args.spp_per_launch,
-                        flags=args.flags, refill=args.refill)
+                        flags=args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0), refill=args.refill)
         if world == 1:
             return st, radiance
         src = radiance if args.dist_backend == "nccl" else radiance.cpu()   # gloo gathers host tensors
@@ -244,7 +246,7 @@ def main():
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
         config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}"
-                              + (" env sky" if args.env else ""),
+                              + (" env sky" if args.env else "") + (" env-IS" if args.env_is else ""),
                   "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
                   "max_depth": args.depth, "seed": args.seed,
                   "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + "

@@ -97,6 +97,9 @@ typedef struct {
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
 #define TPT_FLAG_REF_ORDER     0x2   /* reference right-first traversal, no culling */
+#define TPT_FLAG_ENV_IS        0x8   /* opt-in env next-event estimation with importance sampling (A15
+                                        re-derived; the reference's trace never calls it, so the image
+                                        differs from a reference render) */
 #define TPT_FLAG_ACCUMULATE    0x4   /* progressive: continue the previous call's per-pixel streams and
                                         sums (same frame size, bands and seed); the output is the mean over
                                         all accumulated samples, bit-identical to one call with their total */

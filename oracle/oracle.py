@@ -59,7 +59,7 @@ class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32),
                 ("max_depth", C.c_int32), ("seed", C.c_uint64), ("band_rows", C.c_int32),
                 ("band_count", C.c_int32), ("band_index", C.c_int32), ("trig_mode", C.c_int32),
-                ("threads", C.c_int32)]
+                ("threads", C.c_int32), ("env_is", C.c_int32)]
 
 
 class Counters(C.Structure):
@@ -94,6 +94,9 @@ def lib():
         L.orc_build_bvh.restype = C.c_int
         L.orc_transform.argtypes = [C.POINTER(Scene), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.orc_xorwow_init.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint32)]
+        L.orc_env_is_samples.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_uint64, C.c_int,
+                                         C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.orc_env_is_samples.restype = C.c_int
         L.orc_xorwow_next.argtypes = [C.POINTER(C.c_uint32)]
         L.orc_xorwow_next.restype = C.c_uint32
         L.orc_uniform.argtypes = [C.POINTER(C.c_uint32)]
@@ -198,7 +201,7 @@ def topology_hash(nodes, n_faces):
 
 
 def render(ps: PackedScene, width, height, spp, max_depth=8, seed=42, env=None, trig_mode=1,
-           band_rows=0, band_count=1, band_index=0, threads=0, cam=None):
+           band_rows=0, band_count=1, band_index=0, threads=0, cam=None, env_is=False):
     """Run the oracle frame.  env: (rgba uint8 [h,w,4] row0=bottom) or None.
     Returns (radiance [H,W,3] row0=bottom, bgra [H,W,4] row0=top, counters dict)."""
     s = ps.src
@@ -206,7 +209,8 @@ def render(ps: PackedScene, width, height, spp, max_depth=8, seed=42, env=None, 
     camera.c2w[:] = [float(x) for x in (cam["c2w"] if cam else s.camera_c2w)]
     camera.vfov = float(cam["vfov"] if cam else s.vfov)
     camera.aspect = float(cam["aspect"] if cam else s.aspect)
-    p = Params(width, height, spp, max_depth, seed, band_rows, band_count, band_index, trig_mode, threads)
+    p = Params(width, height, spp, max_depth, seed, band_rows, band_count, band_index, trig_mode, threads,
+               1 if env_is else 0)
     rad = np.zeros((height, width, 3), np.float32)
     bgra = np.zeros((height, width, 4), np.uint8)
     cnt = Counters()
@@ -238,3 +242,16 @@ def uniform_stream(seed, subsequence, n):
 def jump_matrices():
     p = lib().orc_xorwow_jump_matrices()
     return np.ctypeslib.as_array(p, shape=(32 * 160 * 5,)).reshape(32, 160, 5).copy()
+
+
+def env_is_samples(rgba_bottom_up, nf, n, seed=7):
+    """n env importance samples (the build's A15 re-derivation) for normal nf:
+    (dirs [n,3], contribution factors Le*cos/(pi*pdf) [n,3])."""
+    rgba = np.ascontiguousarray(rgba_bottom_up, np.uint8)
+    h, w = rgba.shape[:2]
+    d = np.zeros((n, 3), np.float32)
+    k = np.zeros((n, 3), np.float32)
+    nfa = (C.c_float * 3)(*[float(x) for x in nf])
+    rc = lib().orc_env_is_samples(rgba.ctypes.data, w, h, nfa, seed, n, _ptr(d, C.c_float), _ptr(k, C.c_float))
+    assert rc == 0
+    return d, k

@@ -619,6 +619,104 @@ static inline v3 env_lookup(const orc_env* env, v3 d, int tm) {
     return vscale(1.0f / 255.0f, V3((float)px[0], (float)px[1], (float)px[2]));
 }
 
+/* Env importance sampling: the build's A15 re-derivation (env_light.cu:10-54
+ * intends a 2-D piecewise-constant distribution).  Weight =
+ * luma * sin(theta at the row centre), rows iy = 0 (bottom) .. h-1 as the
+ * lookup reads them, all sums sequential in float. */
+typedef struct {
+    float *w, *cond, *row, *marg;
+    float total;
+} env_is_t;
+
+static void env_is_build(const orc_env* env, env_is_t* t) {
+    const int w = env->w, h = env->h;
+    t->w = (float*)malloc(sizeof(float) * (size_t)w * h);
+    t->cond = (float*)malloc(sizeof(float) * (size_t)w * h);
+    t->row = (float*)malloc(sizeof(float) * (size_t)h);
+    t->marg = (float*)malloc(sizeof(float) * (size_t)h);
+    float acc_rows = 0.0f;
+    for (int iy = 0; iy < h; ++iy) {
+        const float theta = PI_F * (1.0f - ((float)iy + 0.5f) / (float)h);
+        float sw, cw;
+        parity_sincos(theta, &sw, &cw);
+        float acc = 0.0f;
+        for (int ix = 0; ix < w; ++ix) {
+            const uint8_t* px = env->rgba + 4 * ((size_t)iy * w + ix);
+            const float luma = (0.2126f * (float)px[0] + 0.7152f * (float)px[1]) + 0.0722f * (float)px[2];
+            const float wt = luma * sw;
+            t->w[(size_t)iy * w + ix] = wt;
+            acc = acc + wt;
+            t->cond[(size_t)iy * w + ix] = acc;
+        }
+        t->row[iy] = acc;
+        acc_rows = acc_rows + acc;
+        t->marg[iy] = acc_rows;
+    }
+    t->total = acc_rows;
+}
+
+static int lower_bound_f(const float* a, int n, float t) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (a[mid] >= t) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+/* One env sample for a diffuse hit with incident-side normal nf: direction and
+ * the contribution factor Le * cos / (pi * pdf); 0 when it cannot contribute
+ * (the two uniforms are drawn either way). */
+static int env_is_sample(const orc_env* env, const env_is_t* t, v3 nf, uint32_t st[6], int tm, v3* dir, v3* k_le) {
+    const float x1 = orc_uniform(st);
+    const float x2 = orc_uniform(st);
+    const int W = env->w, H = env->h;
+    const float t1 = x1 * t->total;
+    const int iy = lower_bound_f(t->marg, H, t1);
+    const float lo1 = iy > 0 ? t->marg[iy - 1] : 0.0f;
+    const float f1 = fminf((t1 - lo1) / (t->marg[iy] - lo1), 0.99999994f);
+    const float* cond = t->cond + (size_t)iy * W;
+    const float t2 = x2 * t->row[iy];
+    const int ix = lower_bound_f(cond, W, t2);
+    const float lo2 = ix > 0 ? cond[ix - 1] : 0.0f;
+    const float f2 = fminf((t2 - lo2) / (cond[ix] - lo2), 0.99999994f);
+    const float u = ((float)ix + f2) / (float)W;
+    const float v = ((float)iy + f1) / (float)H;
+    float sp, cp, sth, cth;
+    parity_sincos((2.0f * PI_F) * u, &sp, &cp);
+    parity_sincos(PI_F * (1.0f - v), &sth, &cth);
+    *dir = V3(sth * cp, cth, sth * sp);
+    const float c = vdot(*dir, nf);
+    const float pdf = ((t->w[(size_t)iy * W + ix] / t->total) * ((float)W * (float)H)) /
+                      ((2.0f * PI_F * PI_F) * sth);
+    if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < 3.40282347e+38f)) return 0;
+    const v3 le = env_lookup(env, *dir, tm);
+    const float k = c / (PI_F * pdf);
+    *k_le = vscale(k, le);
+    return 1;
+}
+
+/* Test hook: n env samples for normal nf from stream (seed, subsequence 0):
+ * directions and contribution factors (zero when a sample cannot contribute). */
+int orc_env_is_samples(const uint8_t* rgba, int w, int h, const float nf[3], uint64_t seed, int n,
+                       float* dirs, float* k_le) {
+    orc_env env = {rgba, w, h};
+    env_is_t t;
+    env_is_build(&env, &t);
+    if (!(t.total > 0.0f)) { free(t.w); free(t.cond); free(t.row); free(t.marg); return -1; }
+    orc_xorwow_jump_matrices();
+    uint32_t st[6];
+    orc_xorwow_init(seed, 0, st);
+    for (int i = 0; i < n; ++i) {
+        v3 d = V3(0.0f, 0.0f, 0.0f), k = V3(0.0f, 0.0f, 0.0f);
+        if (!env_is_sample(&env, &t, V3(nf[0], nf[1], nf[2]), st, 1, &d, &k)) k = V3(0.0f, 0.0f, 0.0f);
+        dirs[3 * i] = d.x; dirs[3 * i + 1] = d.y; dirs[3 * i + 2] = d.z;
+        k_le[3 * i] = k.x; k_le[3 * i + 1] = k.y; k_le[3 * i + 2] = k.z;
+    }
+    free(t.w); free(t.cond); free(t.row); free(t.marg);
+    return 0;
+}
+
 static const orc_material k_default_material = {
     {0.82f, 0.67f, 0.16f}, 0.0f, 0.0f, 0.0f, 0.0f, 0.5f, 0.5f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 1.0f};
 
@@ -629,6 +727,7 @@ typedef struct {
     const float* c2w;
     float vfov, aspect, tan_half;
     int W, H, spp, max_depth, tm;
+    const env_is_t* is;   /* non-NULL: env next-event estimation (opt-in A15) */
 } trace_ctx;
 
 static inline const orc_material* mtl_of(const trace_ctx* c, int fid) {
@@ -699,6 +798,16 @@ static void trace_pixel(const trace_ctx* c, int px, int py, uint32_t st[6], floa
                 hit_t sh2;
                 traverse(&c->b, &sr, &sh2, cnt);
                 if (sh2.hit == -1) direct = vadd(direct, vmul(base, lrad));
+            }
+            if (c->is && !(m->eta > 0.0f) && !(m->metallic > 0.0f)) {   /* env NEE (opt-in) */
+                float sgn = vdot(ray.d, nrm) > 0.0f ? -1.0f : 1.0f;     /* getNewDirection's flip */
+                v3 edir, ek;
+                if (env_is_sample(c->env, c->is, vscale(sgn, nrm), st, c->tm, &edir, &ek)) {
+                    ray_t sr = {ray.o, edir};
+                    hit_t sh3;
+                    traverse(&c->b, &sr, &sh3, cnt);
+                    if (sh3.hit == -1) direct = vadd(direct, ek);
+                }
             }
             if (!(m->eta >= 1.0f || m->metallic > 0.0f)) {  /* direct probe :387-401 */
                 v3 pdir;
@@ -778,6 +887,12 @@ int orc_render(const orc_scene* s, const orc_env* env, const orc_camera* cam, co
     c.s = s; c.env = env; c.c2w = cam->c2w; c.vfov = cam->vfov; c.aspect = cam->aspect;
     c.W = W; c.H = H; c.spp = p->spp; c.max_depth = p->max_depth; c.tm = p->trig_mode;
     c.tan_half = t_tan(p->trig_mode, cam->vfov * 0.5f);
+    env_is_t is_tab = {NULL, NULL, NULL, NULL, 0.0f};
+    c.is = NULL;
+    if (p->env_is && env && env->rgba) {
+        env_is_build(env, &is_tab);
+        if (is_tab.total > 0.0f) c.is = &is_tab;
+    }
 
 #ifdef _OPENMP
     if (p->threads > 0) omp_set_num_threads(p->threads);
@@ -828,5 +943,6 @@ int orc_render(const orc_scene* s, const orc_env* env, const orc_camera* cam, co
         out->init_ms = t1 - t0; out->trace_ms = t2 - t1;
     }
     free(wv); free(wn); free(nodes); free(keys); free(states);
+    free(is_tab.w); free(is_tab.cond); free(is_tab.row); free(is_tab.marg);
     return 0;
 }

@@ -84,12 +84,19 @@ typedef struct {
     int32_t trig_mode;    /* 0: libm float functions (as the survey harness);
                              1: parity trig, bit-identical to the HIP kernel */
     int32_t threads;      /* OpenMP threads, 0 = default */
+    int32_t env_is;       /* 1: env next-event estimation with importance sampling (the
+                             build's opt-in A15 re-derivation, TPT_FLAG_ENV_IS) */
 } orc_params;
 
 typedef struct {
     uint64_t traversals, internal_visits, leaf_tests, shade_hits, pixels;
     double init_ms, trace_ms;
 } orc_counters;
+
+/* Env importance sampling (the build's A15 re-derivation): n samples for
+ * incident-side normal nf, stream (seed, 0); dirs/k_le are n*3 floats. */
+int orc_env_is_samples(const uint8_t* rgba, int w, int h, const float nf[3], uint64_t seed, int n,
+                       float* dirs, float* k_le);
 
 /* cuRAND XORWOW restatement (curand_init / curand / curand_uniform). */
 void orc_xorwow_init(uint64_t seed, uint64_t subsequence, uint32_t state[6]);

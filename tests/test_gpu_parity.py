@@ -182,6 +182,29 @@ def test_render_parity(built, name, W, H, spp, depth, env, order):
             assert stats["leaf_tests"] <= oc["leaf_tests"]
 
 
+@pytest.mark.parametrize("name", ["ball", "box1", "box"])
+def test_env_importance_sampling_parity(built, name):
+    """TPT_FLAG_ENV_IS (A15 re-derived, opt-in): env next-event estimation at
+    diffuse hits against the oracle's restatement -- same tables, samples,
+    shadow rays and ray counts; and the flag does change the image."""
+    s, d, o = built[name]
+    W, H, spp = 48, 27, 8
+    sky = T.procedural_sky(128, 64)
+    pt = T.PathTracer("", W, H, 0)
+    pt.envLight = T.EnvLight(sky, 0)
+    rad = np.zeros((H, W, 3), np.float32)
+    stats = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=rad, flags=T._lib.FLAG_ENV_IS)
+    orad, _, oc = O.render(o, W, H, spp, 8, 42, env=sky[::-1].copy(), trig_mode=1, env_is=True)
+    m = image_metrics(rad, orad)
+    assert_parity(m)
+    if m["bit_same"] == 1.0:
+        assert stats["traversals"] == oc["traversals"]
+    plain = np.zeros((H, W, 3), np.float32)
+    st2 = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=plain)
+    assert st2["traversals"] < stats["traversals"]        # one env shadow ray per diffuse hit
+    assert not np.array_equal(_bits(plain), _bits(rad))
+
+
 def test_band_sharding_bit_identical(built):
     s, d, _ = built["box"]
     W, H, spp = 64, 48, 8

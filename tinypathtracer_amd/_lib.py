@@ -17,6 +17,7 @@ STATUS_NAMES = {0: "OK", 1: "INVALID_ARG", 2: "HIP_ERROR", 3: "OOM", 4: "IO", 5:
 FLAG_NO_COUNTERS = 0x1
 FLAG_REF_ORDER = 0x2
 FLAG_ACCUMULATE = 0x4
+FLAG_ENV_IS = 0x8
 
 
 class Material(C.Structure):

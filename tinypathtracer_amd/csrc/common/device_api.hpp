@@ -53,6 +53,12 @@ struct TraceArgs {
     // env (nullable)
     const uint32_t* env;                 // RGBA8 packed, row 0 = bottom
     int32_t env_w, env_h;
+    const float* is_w;                   // env importance sampling (A15): texel weights [h][w]
+    const float* is_cond;                //   row prefix sums [h][w]
+    const float* is_row;                 //   row sums [h]
+    const float* is_marg;                //   marginal prefix over rows [h]
+    float is_total;
+    int32_t env_is;                      // TPT_FLAG_ENV_IS and a non-empty distribution
     // camera
     float c2w[16];
     float origin[3];                     // c2w * (0,0,0,1)

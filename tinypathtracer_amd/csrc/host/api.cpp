@@ -17,7 +17,9 @@
 #include <vector>
 
 #include "../common/device_api.hpp"
+#include "../common/ptrig.hpp"
 #include "../common/rng.hpp"
+#include "../common/tpt_math.hpp"
 #include "tpt.h"
 #include "tpt_internal.hpp"
 
@@ -111,7 +113,48 @@ struct tpt_env {
     int device = 0;
     int w = 0, h = 0;
     DevBuf<uint32_t> texels;
+    // importance-sampling tables (A15, TPT_FLAG_ENV_IS): per-texel weight, row
+    // prefix sums, row sums, marginal prefix over rows; total <= 0 disables
+    DevBuf<float> is_w, is_cond, is_row, is_marg;
+    float is_total = 0.0f;
 };
+
+namespace {
+
+// A15 re-derivation (env_light.cu:10-54 intends a 2-D piecewise-constant
+// distribution; its weight uses theta for sin(theta), its normalisation races
+// across blocks and its row orientation is the reverse of Vec2UV).  Here:
+// w = luma * sin(theta at the row centre), rows iy = 0 (bottom) .. h-1 as the
+// lookup reads them (v = 1 - acos(y)/pi), all sums sequential in float --
+// the oracle builds the same tables with the same operations.
+void build_env_is(const uint8_t* rgba, int w, int h, std::vector<float>& W, std::vector<float>& cond,
+                  std::vector<float>& row, std::vector<float>& marg, float& total) {
+    W.resize((size_t)w * h);
+    cond.resize((size_t)w * h);
+    row.resize(h);
+    marg.resize(h);
+    float acc_rows = 0.0f;
+    for (int iy = 0; iy < h; ++iy) {
+        const float theta = tpt::kPi * (1.0f - ((float)iy + 0.5f) / (float)h);
+        float sw, cw;
+        tpt::fsincos_2pi(theta, sw, cw);
+        float acc = 0.0f;
+        for (int ix = 0; ix < w; ++ix) {
+            const uint8_t* px = rgba + 4 * ((size_t)iy * w + ix);
+            const float luma = (0.2126f * (float)px[0] + 0.7152f * (float)px[1]) + 0.0722f * (float)px[2];
+            const float wt = luma * sw;
+            W[(size_t)iy * w + ix] = wt;
+            acc = acc + wt;
+            cond[(size_t)iy * w + ix] = acc;
+        }
+        row[iy] = acc;
+        acc_rows = acc_rows + acc;
+        marg[iy] = acc_rows;
+    }
+    total = acc_rows;
+}
+
+}  // namespace
 
 struct tpt_scene {
     int device = 0;
@@ -344,6 +387,13 @@ tpt_status tpt_env_create(const uint8_t* rgba, int32_t w, int32_t h, int device,
     env->h = h;
     hipError_t e = env->texels.alloc((size_t)w * (size_t)h);
     if (e == hipSuccess) e = hipMemcpy(env->texels.p, rgba, (size_t)w * h * 4, hipMemcpyHostToDevice);
+    std::vector<float> iw, icond, irow, imarg;
+    build_env_is(rgba, w, h, iw, icond, irow, imarg, env->is_total);
+    if (e == hipSuccess) e = env->is_w.upload(iw.data(), iw.size(), nullptr);
+    if (e == hipSuccess) e = env->is_cond.upload(icond.data(), icond.size(), nullptr);
+    if (e == hipSuccess) e = env->is_row.upload(irow.data(), irow.size(), nullptr);
+    if (e == hipSuccess) e = env->is_marg.upload(imarg.data(), imarg.size(), nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         delete env;
         return fail(TPT_ERR_HIP, std::string("env upload: ") + hipGetErrorString(e));
@@ -374,6 +424,11 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.env = env ? env->texels.p : nullptr;
     a.env_w = env ? env->w : 0;
     a.env_h = env ? env->h : 0;
+    a.is_w = env ? env->is_w.p : nullptr;
+    a.is_cond = env ? env->is_cond.p : nullptr;
+    a.is_row = env ? env->is_row.p : nullptr;
+    a.is_marg = env ? env->is_marg.p : nullptr;
+    a.is_total = env ? env->is_total : 0.0f;
     if (cam) {
         std::memcpy(a.c2w, cam->c2w, sizeof a.c2w);
         float r[4];
@@ -439,6 +494,8 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     a.band_height = bh;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
+    // A15 env next-event estimation: opt-in, needs an env with a non-empty distribution
+    a.env_is = ((p->flags & TPT_FLAG_ENV_IS) && env && env->is_total > 0.0f) ? 1 : 0;
     a.refill = p->refill > 0 ? std::min(p->refill, 64) : 24;
     a.rng = s->rng.p;
     a.accum = s->accum.p;

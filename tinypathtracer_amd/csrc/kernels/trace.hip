@@ -471,7 +471,53 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {
     return s;
 }
 
-enum : int { PH_CAMERA = 0, PH_EXT = 1, PH_SHADOW = 2, PH_PROBE = 3 };
+enum : int { PH_CAMERA = 0, PH_EXT = 1, PH_SHADOW = 2, PH_PROBE = 3, PH_ENVSHADOW = 4 };
+
+// A15 env importance sampling, re-derived (TPT_FLAG_ENV_IS): a
+// texel by the marginal (rows) then conditional (columns) CDF, the remapped
+// uniforms as the position inside it, a direction by the inverse of Vec2UV
+// (env_light.cuh:72-78) and its solid-angle pdf.  Returns the contribution
+// factor Le * cos / (pi * pdf) for a diffuse hit with incident-side normal nf,
+// or false when the sample cannot contribute (the two uniforms are drawn
+// either way).  The oracle's env_is_sample is the same arithmetic.
+__device__ __forceinline__ int lower_bound_f(const float* __restrict__ a, int n, float t) {
+    int lo = 0, hi = n - 1;   // first i with a[i] >= t (n - 1 if none)
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a[mid] >= t) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+__device__ __noinline__ bool env_is_sample(const TraceArgs& a, V3 nf, uint32_t st[6], V3& dir, V3& k_le) {
+    const float x1 = xorwow_uniform(st);
+    const float x2 = xorwow_uniform(st);
+    const int W = a.env_w, H = a.env_h;
+    const float t1 = x1 * a.is_total;
+    const int iy = lower_bound_f(a.is_marg, H, t1);
+    const float lo1 = iy > 0 ? a.is_marg[iy - 1] : 0.0f;
+    const float f1 = fminf((t1 - lo1) / (a.is_marg[iy] - lo1), 0.99999994f);
+    const float* cond = a.is_cond + (size_t)iy * (size_t)W;
+    const float t2 = x2 * a.is_row[iy];
+    const int ix = lower_bound_f(cond, W, t2);
+    const float lo2 = ix > 0 ? cond[ix - 1] : 0.0f;
+    const float f2 = fminf((t2 - lo2) / (cond[ix] - lo2), 0.99999994f);
+    const float u = ((float)ix + f2) / (float)W;
+    const float v = ((float)iy + f1) / (float)H;
+    float sp, cp, sth, cth;
+    fsincos_2pi((2.0f * kPi) * u, sp, cp);
+    fsincos_2pi(kPi * (1.0f - v), sth, cth);
+    dir = v3(sth * cp, cth, sth * sp);
+    const float c = dot(dir, nf);
+    const float pdf = ((a.is_w[(size_t)iy * (size_t)W + ix] / a.is_total) * ((float)W * (float)H)) /
+                      ((2.0f * kPi * kPi) * sth);
+    if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < kRealMax)) return false;
+    const V3 le = env_lookup(a.env, W, H, dir);
+    const float k = c / (kPi * pdf);
+    k_le = k * le;
+    return true;
+}
 enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2 };
 
 // Per-lane path records (path_tracer.cu:315-318), consumed by the unwind
@@ -524,7 +570,7 @@ struct PathRecords {
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
 // state (direct term, normal, light index, incoming direction -- r.d during an
 // extension ray) is dead across traversals and drops out of the registers.
-template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT>
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false>
 __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -587,6 +633,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     int phase = PH_CAMERA;
     int depth = 0, li = 0;
     uint32_t mk = 0;   // material id | p-kind << 30 of the current bounce
+    bool env_pending = false;   // A15: this bounce's env next-event sample is still to be drawn
+    V3 env_k = v3(0.0f, 0.0f, 0.0f);
     V3 rd = v3(0.0f, 0.0f, 0.0f), nd = rd, nrm = rd, direct = rd;
     Trav r;
     trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), false);
@@ -631,6 +679,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     mk = (uint32_t)mtl | (p_kind(prob) << 30);
                     direct = v3(0.0f, 0.0f, 0.0f);
                     li = 0;
+                    env_pending = ENVIS && !(m1.x > 0.0f) && !(m1.y > 0.0f);   // diffuse hit
                     lights_next = true;
                 }
             } else if (LIGHTS && phase == PH_SHADOW) {
@@ -641,6 +690,9 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     direct = direct + (v3(m0.x, m0.y, m0.z) * lrad);
                 }
                 ++li;
+                lights_next = true;
+            } else if (ENVIS && phase == PH_ENVSHADOW) {   // env next-event estimate (A15, opt-in)
+                if (r.fid < 0) direct = direct + env_k;
                 lights_next = true;
             } else if (phase == PH_PROBE) {   // :390-400
                 V3 dl = LIGHTS ? direct : v3(0.0f, 0.0f, 0.0f);
@@ -662,13 +714,26 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     light_sample(a.lights, li, r.o, td, lrad);
                     phase = PH_SHADOW;
                     shadow = true;
-                } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
-                    float af2;
-                    new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
-                    phase = PH_PROBE;
                 } else {
-                    rec.put_dst(depth, mk, kNoProbe, direct);
-                    after = true;
+                    bool env_ray = false;
+                    if (ENVIS && env_pending) {   // after the delta lights, before the probe
+                        env_pending = false;
+                        const V3 nf = (dot(rd, nrm) > 0.0f ? -1.0f : 1.0f) * nrm;   // getNewDirection's flip
+                        if (env_is_sample(a, nf, st, td, env_k)) {
+                            phase = PH_ENVSHADOW;
+                            shadow = true;
+                            env_ray = true;
+                        }
+                    }
+                    if (env_ray) {
+                    } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
+                        float af2;
+                        new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
+                        phase = PH_PROBE;
+                    } else {
+                        rec.put_dst(depth, mk, kNoProbe, direct);
+                        after = true;
+                    }
                 }
             }
             if (after) {
@@ -924,9 +989,9 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
     }
 }
 
-template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT>
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false>
 static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS>), grid, dim3(256), lds, s, a);
 }
 
 template <bool LIGHTS, bool MTL_LDS, typename StackT>
@@ -979,6 +1044,13 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
         // the reference's visit order (tests, diagnostics): one general variant
         const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, false);
         launch_one<64, false, true, false, int>(a, grid, lds, s);
+        return hipGetLastError();
+    }
+    if (a.env_is) {
+        // opt-in env next-event estimation (A15): one general variant (delta
+        // lights machinery, 32-bit stack, any depth) keeps the others lean
+        const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, true);
+        launch_one<64, true, true, false, int, true>(a, grid, lds, s);
         return hipGetLastError();
     }
     const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
