@@ -13,11 +13,19 @@
 //    traversal state in registers -- the wave pays the average traversal length
 //    of its lanes, not the longest, and every pixel still consumes its own
 //    XORWOW stream in the reference's order;
-//  * LDS per lane: the traversal stack ([slot][lane], 16-bit node ids when the
-//    tree allows) and the path records of the first two bounces; deeper records
-//    spill to private memory (rare);
-//  * node records are 64 B (both child AABBs + links: one visit = four 16-B
-//    loads), triangles are pre-gathered (v0, e1, e2, fid: three 16-B loads).
+//  * ordered traversal over 4-wide nodes (the even-depth nodes of the binary
+//    LBVH, 128 B: seven 16-B loads per visit) with an exact min/max slab test
+//    for finite rays, and speculative leaf postponement; the binary nodes and
+//    the reference's ternary slab test serve the reference visit order and
+//    rays with a non-finite origin or 1/dir;
+//  * LDS per workgroup: the material table, the traversal stack ([slot][lane],
+//    16-bit ids when the tree allows; deepest slots private when it does not
+//    fit) and as many path-record levels as fit (2 words per bounce without
+//    delta lights); deeper records in private memory;
+//  * kernel variants by template: no-lights / delta lights, material table in
+//    LDS or not, 16/32-bit stack ids, record depth 8/64; the reference order
+//    and the opt-in env importance sampling have one general variant each;
+//  * triangles are pre-gathered (v0, e1, e2, fid: three 16-B loads).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -170,22 +178,6 @@ __device__ __forceinline__ void slab_minmax(const V3& o, const V3& inv, float nx
     t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
 }
 
-__device__ __forceinline__ void inner_visit_fast(const Trav& r, const float4* __restrict__ inner, int& next,
-                                                 bool& push, int& deferred) {
-    const float4* nd = inner + 4 * r.node;
-    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-    float l0, l1, r0, r1;
-    slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
-    slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
-    const float hi = fminf(kRealMax, r.t * 1.0001f);
-    const bool hl = fmaxf(l0, 0.5f * kDelta) <= fminf(l1, hi);
-    const bool hr = fmaxf(r0, 0.5f * kDelta) <= fminf(r1, hi);
-    const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
-    const bool lfirst = l0 < r0;
-    push = hl & hr;
-    deferred = lfirst ? rc : lc;
-    next = push ? (lfirst ? lc : rc) : (hl ? lc : (hr ? rc : -1));
-}
 
 // Traversal stack of one lane: slots [0, nlds) in LDS ([slot][lane], shared
 // memory of the workgroup), deeper slots in private memory.  Deep stacks are
@@ -438,20 +430,12 @@ __device__ __forceinline__ void light_sample(const DevLight* __restrict__ Ls, in
 
 // sampleEnvLights (:288-294): Vec2UV (env_light.cuh:72-78) + point/clamp fetch
 // (texture.cu:156-170) of the RGBA8 equirect, row 0 = bottom.
-#ifdef TPT_EXP_ENV_INLINE
-#define TPT_ENV_ATTR __forceinline__
-#else
-#define TPT_ENV_ATTR __noinline__
-#endif
-__device__ TPT_ENV_ATTR V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
-#ifdef TPT_EXP_NO_ENV_TRIG   // timing-only knock-out: wrong texels
-    float u = d.z * 0.5f + 0.5f;
-    const float v = d.y * 0.5f + 0.5f;
-#else
+// (kept out of line: inlined, its double-precision trig raised the register
+// pressure of the whole kernel; C3 measured 17 % slower)
+__device__ __noinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
     float u = patan2_fast(d.z, d.x) / (2.0f * kPi);
     if (u < 0.0f) u += 1.0f;
     const float v = 1.0f - pacos_fast(fclamp(d.y, 1.0f, -1.0f)) / kPi;
-#endif
     int ix = (int)floorf(u * (float)w);
     int iy = (int)floorf(v * (float)h);
     ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
