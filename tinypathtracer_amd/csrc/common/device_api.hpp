@@ -5,7 +5,9 @@
 //       q0 = (L.min.xyz, L.max.x)  q1 = (L.max.yz, R.min.xy)
 //       q2 = (R.min.z, R.max.xyz)  q3 = (bits(left), bits(right), 0, 0)
 //     child ids use the reference numbering (bvh.cu:164-214): id >= F-1 is
-//     the leaf at sorted position id-(F-1).
+//     the leaf at sorted position id-(F-1).  Bit 30 of every child link is
+//     set when that child's subtree holds an emissive triangle (inner and
+//     inner4); traversals mask it off.
 //   inner4[8*n4] float4  4-wide view for the ordered traversal: one node per
 //     even-depth internal node, numbered breadth-first (root 0), holding its up
 //     to 4 grandchildren (a leaf child stands for itself): child k box = floats
@@ -137,6 +139,7 @@ struct BuildBuffers {
     uint32_t* bfs_ids;                   // F-1
     uint32_t* bfs_ids_sorted;
     uint32_t* bfs_newid;                 // F-1: binary id -> breadth-first 4-wide id
+    uint32_t* emit;                      // 2F-1: subtree holds an emissive triangle
     void* sort_tmp;
     size_t sort_tmp_bytes;
     // outputs

@@ -176,7 +176,7 @@ struct tpt_scene {
     // world + BVH
     DevBuf<float> wverts, wnorms, leaf_box, node_box;
     DevBuf<unsigned long long> keys, keys_sorted, bfs_keys, bfs_keys_sorted;
-    DevBuf<uint32_t> fids, fids_sorted, parent, flags, max_depth, bfs_ids, bfs_ids_sorted, bfs_newid;
+    DevBuf<uint32_t> fids, fids_sorted, parent, flags, max_depth, bfs_ids, bfs_ids_sorted, bfs_newid, emit;
     DevBuf<int2> children;
     DevBuf<uint8_t> sort_tmp, nodes36;
     DevBuf<float4> inner, inner4, tri, shade;
@@ -313,6 +313,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     HIP_OR_FAIL(s->bfs_ids.alloc(std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->bfs_ids_sorted.alloc(std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->bfs_newid.alloc(std::max<size_t>(n - 1, 1)));
+    HIP_OR_FAIL(s->emit.alloc(nn));
     HIP_OR_FAIL(s->sort_tmp.alloc(std::max<size_t>(sort_bytes, 16)));
     HIP_OR_FAIL(s->inner.alloc(4 * std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->inner4.alloc(8 * std::max<size_t>(n - 1, 1)));
@@ -354,6 +355,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     b.bfs_ids = s->bfs_ids.p;
     b.bfs_ids_sorted = s->bfs_ids_sorted.p;
     b.bfs_newid = s->bfs_newid.p;
+    b.emit = s->emit.p;
     b.tri = s->tri.p;
     b.shade = s->shade.p;
     b.nodes36 = s->nodes36.p;

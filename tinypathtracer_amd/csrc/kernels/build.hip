@@ -154,10 +154,16 @@ __global__ void k_depth(BuildBuffers b, uint32_t* depth) {
     const int id = blockIdx.x * blockDim.x + threadIdx.x;
     if (id >= nn) return;
     if (id >= n - 1) {
-        const float* src = b.leaf_box + 6 * b.fids_sorted[id - (n - 1)];
+        const uint32_t fid = b.fids_sorted[id - (n - 1)];
+        const float* src = b.leaf_box + 6 * fid;
         float* dst = b.node_box + 6 * id;
 #pragma unroll
         for (int k = 0; k < 6; ++k) dst[k] = src[k];
+        // emitter flag of the leaf: its material's emissionFactor != 0 (the
+        // direct probe only needs the closest emissive hit, see trace.hip)
+        int mtl = b.lut[find_object((int)fid, b.lut, b.n_objects)].y;
+        if (mtl < 0 || mtl >= b.n_materials) mtl = b.n_materials;   // Material() slot
+        b.emit[id] = b.mtl[2 * mtl].w != 0.0f ? 1u : 0u;
     }
     uint32_t d = 0;
     int cur = id;
@@ -179,6 +185,12 @@ __global__ void k_union_level(BuildBuffers b, const uint32_t* __restrict__ depth
     float* o = b.node_box + 6 * i;
     o[0] = fmn(l[0], r[0]); o[1] = fmn(l[1], r[1]); o[2] = fmn(l[2], r[2]);
     o[3] = fmx(l[3], r[3]); o[4] = fmx(l[4], r[4]); o[5] = fmx(l[5], r[5]);
+    b.emit[i] = b.emit[c.x] | b.emit[c.y];   // subtree holds an emissive triangle
+}
+
+// Child links carry the child's emitter flag in bit 30 (ids < 2^30).
+__device__ __forceinline__ int link(const BuildBuffers& b, int id) {
+    return id < 0 ? id : (id | (int)(b.emit[id] << 30));
 }
 
 __global__ void k_pack_inner(BuildBuffers b) {
@@ -191,7 +203,7 @@ __global__ void k_pack_inner(BuildBuffers b) {
     q[0] = make_float4(l[0], l[1], l[2], l[3]);
     q[1] = make_float4(l[4], l[5], r[0], r[1]);
     q[2] = make_float4(r[2], r[3], r[4], r[5]);
-    q[3] = make_float4(__int_as_float(c.x), __int_as_float(c.y), 0.0f, 0.0f);
+    q[3] = make_float4(__int_as_float(link(b, c.x)), __int_as_float(link(b, c.y)), 0.0f, 0.0f);
     bool fin = true;
 #pragma unroll
     for (int k = 0; k < 6; ++k) fin = fin && isfinite(l[k]) && isfinite(r[k]);
@@ -248,7 +260,8 @@ __global__ void k_pack_inner4(BuildBuffers b, const uint32_t* __restrict__ depth
     int out[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)   // internal grandchildren -> breadth-first id; leaves keep nint + position
-        out[k] = (ids[k] >= 0 && ids[k] < nint) ? (int)b.bfs_newid[ids[k]] : ids[k];
+        out[k] = (ids[k] >= 0 && ids[k] < nint) ? ((int)b.bfs_newid[ids[k]] | (int)(b.emit[ids[k]] << 30))
+                                                : link(b, ids[k]);
     q[6] = make_float4(__int_as_float(out[0]), __int_as_float(out[1]), __int_as_float(out[2]),
                        __int_as_float(out[3]));
     q[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);

@@ -109,19 +109,33 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 //    before Delta/2 -- boxes that cannot hold an accepted hit.  Exact ties
 //    (t == best) resolve to the larger leaf position, the triangle the
 //    reference's right-first DFS meets first, so the winner is the reference's.
-//  any_hit: shadow rays stop at the first accepted triangle (only hitIdx == -1
-//    matters, :279).
+//  Modes:
+//   TM_CLOSEST  closest hit (extension and camera rays; probes in reference order)
+//   TM_ANY      shadow rays stop at the first accepted triangle (only
+//               hitIdx == -1 matters, :279)
+//   TM_EMIT     direct probe, pass 1: the closest hit among emissive triangles
+//               only -- children whose subtree holds no emitter (bit 30 of the
+//               link) are not entered
+//   TM_OCCL     direct probe, pass 2 (after an emitter hit): any triangle that
+//               beats that hit (t, then leaf position) ends the ray as
+//               TM_OCCLUDED.  The probe only reads the closest hit's emission
+//               (:394-396): an emitter hit nothing beats is the closest hit; if
+//               something beats it, that triangle's emission is 0 and adds
+//               exactly like a miss (the direct term is never -0).
 // ---------------------------------------------------------------------------
+enum : int { TM_CLOSEST = 0, TM_ANY = 1, TM_EMIT = 2, TM_OCCL = 3, TM_OCCLUDED = 4 };
+constexpr int kLinkMask = 0x3fffffff;   // child link without its emitter bit
+
 struct Trav {
     V3 o, d, inv;
     int node, sp, hpos, fid;
     int pend;   // parked leaf position (speculative traversal), -1: none
     float t, u, v;
-    bool any_hit;
+    int mode;   // TM_*
     bool fin;   // origin and 1/dir finite: no slab product can be NaN
 };
 
-__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit, bool boxes_finite = false) {
+__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool boxes_finite = false) {
     r.o = o;
     r.d = d;
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
@@ -133,7 +147,7 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, bool any_hit, bo
     r.t = kRealMax;
     r.u = 0.0f;
     r.v = 0.0f;
-    r.any_hit = any_hit;
+    r.mode = mode;
     r.fin = boxes_finite & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
             __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
 }
@@ -148,11 +162,16 @@ __device__ __forceinline__ void inner_visit(const Trav& r, const float4* __restr
     float l0, l1, r0, r1;
     bool hl = box_hit(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, l0, l1);
     bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
-    const int lc = __float_as_int(q3.x), rc = __float_as_int(q3.y);
+    const int lraw = __float_as_int(q3.x), rraw = __float_as_int(q3.y);
+    const int lc = lraw & kLinkMask, rc = rraw & kLinkMask;
     if (ORDERED) {
         const float lim = r.t * 1.0001f;
         hl = hl & !(l0 > lim) & !(l1 < 0.5f * kDelta);
         hr = hr & !(r0 > lim) & !(r1 < 0.5f * kDelta);
+        if (r.mode == TM_EMIT) {   // probe pass 1: emitter subtrees only
+            hl = hl & ((lraw >> 30) != 0);
+            hr = hr & ((rraw >> 30) != 0);
+        }
     }
     const bool lfirst = ORDERED && (l0 < r0);   // reference order: right child first
     push = hl & hr;
@@ -243,10 +262,16 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
     const float hi = fminf(kRealMax, r.t * 1.0001f);
     int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z), i3 = __float_as_int(q6.w);
     const float hd = 0.5f * kDelta;
-    const bool h0 = (i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi));
-    const bool h1 = (i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi));
-    const bool h2 = (i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi));
-    const bool h3 = (i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi));
+    // a link is -1 (no child) or an id with the emitter flag in bit 30
+    const int need = r.mode == TM_EMIT ? (1 << 30) : 0;   // probe pass 1: emitter subtrees only
+    const bool h0 = (i0 >= 0) & ((i0 & need) == need) & (fmaxf(k0, hd) <= fminf(e0, hi));
+    const bool h1 = (i1 >= 0) & ((i1 & need) == need) & (fmaxf(k1, hd) <= fminf(e1, hi));
+    const bool h2 = (i2 >= 0) & ((i2 & need) == need) & (fmaxf(k2, hd) <= fminf(e2, hi));
+    const bool h3 = (i3 >= 0) & ((i3 & need) == need) & (fmaxf(k3, hd) <= fminf(e3, hi));
+    i0 &= kLinkMask;
+    i1 &= kLinkMask;
+    i2 &= kLinkMask;
+    i3 &= kLinkMask;
     const float inf = __builtin_inff();
     k0 = h0 ? k0 : inf;
     k1 = h1 ? k1 : inf;
@@ -312,7 +337,9 @@ __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tr
     r.u = take ? u : r.u;
     r.v = take ? v : r.v;
     r.hpos = take ? pos : r.hpos;
-    return take & r.any_hit;
+    const bool occl = r.mode == TM_OCCL;
+    r.mode = (take & occl) ? TM_OCCLUDED : r.mode;
+    return take & ((r.mode == TM_ANY) | occl);
 }
 
 // Returns false once the traversal has finished (or overflowed its stack).
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     V3 env_k = v3(0.0f, 0.0f, 0.0f);
     V3 rd = v3(0.0f, 0.0f, 0.0f), nd = rd, nrm = rd, direct = rd;
     Trav r;
-    trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), false);
+    trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), TM_CLOSEST);
     int ts = active ? TS_DONE : TS_DEAD;
     const int refill = a.refill;
 
@@ -638,6 +665,15 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             t_iter0 = now;
         }
 #endif
+        if (ORDERED && ts == TS_DONE && phase == PH_PROBE && r.mode == TM_EMIT && r.fid >= 0) {
+            // direct probe, pass 2: the emitter hit stands unless something
+            // beats it -- restart from the root keeping its t, position and fid
+            r.mode = TM_OCCL;
+            r.node = 0;
+            r.sp = 0;
+            r.pend = -1;
+            ts = TS_TRAV;
+        }
         if (ts == TS_DONE) {
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
@@ -681,7 +717,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             } else if (phase == PH_PROBE) {   // :390-400
                 V3 dl = LIGHTS ? direct : v3(0.0f, 0.0f, 0.0f);
                 uint32_t pm = kNoProbe;
-                if (r.fid >= 0) {
+                if (r.fid >= 0 && r.mode != TM_OCCLUDED) {   // the closest hit (an unbeaten emitter, pass 2)
                     pm = (uint32_t)__float_as_int(a.shade[3 * r.fid].w);
                     const float e = MT(2 * pm).w;
                     dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + dl;
@@ -801,7 +837,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
 #endif
             if (ts != TS_DEAD) {
                 ++c_trav;
-                trav_begin(r, to, td, shadow, a.boxes_finite != 0);
+                trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
+                           a.boxes_finite != 0);
                 ts = TS_TRAV;
             }
         }
@@ -962,7 +999,8 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
     uint32_t c0 = 0, c1 = 0, c2 = 0;
     if (i < n) {
         Trav r;
-        trav_begin(r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]), false);
+        trav_begin(r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                   TM_CLOSEST);
         while (trav_step<false>(r, a.inner, a.tri, a.n_faces - 1, (int*)lds + threadIdx.x, a.stack_depth, c0, c1,
                                 c2)) {
         }
