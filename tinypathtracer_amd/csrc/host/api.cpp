@@ -164,6 +164,7 @@ struct tpt_scene {
     bool built = false;
     int32_t stack_depth = 0;
     int32_t boxes_finite = 0;
+    int32_t any_emitter = 1;                // some triangle's material has emissionFactor != 0
     int32_t n4 = 0;
     uint32_t tree_depth = 0;
     // inputs
@@ -363,6 +364,12 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     s->tree_depth = b.out_max_depth;
     s->boxes_finite = (int32_t)b.out_boxes_finite;
     s->n4 = (int32_t)b.out_n4;
+    {   // the root's emitter flag: does any triangle emit (a probe can only add emission)
+        uint32_t root_emit = 1;
+        HIP_OR_FAIL(hipMemcpyAsync(&root_emit, s->emit.p, sizeof root_emit, hipMemcpyDeviceToHost, s->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+        s->any_emitter = root_emit != 0 ? 1 : 0;
+    }
     // Stack capacity: the binary DFS that pushes one sibling per level holds at
     // most depth + 1 entries; the 4-wide ordered traversal pushes up to 3 per
     // 4-wide node, one per two levels: 3 * ceil(depth / 2).
@@ -423,6 +430,7 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.lights = s->lights.p;
     a.stack_depth = s->stack_depth;
     a.boxes_finite = s->boxes_finite;
+    a.any_emitter = s->any_emitter;
     a.env = env ? env->texels.p : nullptr;
     a.env_w = env ? env->w : 0;
     a.env_h = env ? env->h : 0;
@@ -471,9 +479,9 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     s->acc_valid = false;   // re-armed once this call has completed
     HIP_OR_FAIL(s->rng.alloc(6 * npix));
     HIP_OR_FAIL(s->accum.alloc(3 * npix));
-    HIP_OR_FAIL(s->counters.alloc(16));
+    HIP_OR_FAIL(s->counters.alloc(32));
     if (!resume) HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * sizeof(float), st));   // thrust::fill (:534)
-    HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 16 * sizeof(unsigned long long), st));
+    HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 32 * sizeof(unsigned long long), st));
 
     // setupRandSeed (:513); a progressive call continues the persisted streams
     HIP_OR_FAIL(hipEventRecord(s->ev[0], st));
@@ -573,7 +581,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
                                    st));
     if (bgra_out && !bgra_dev)
         HIP_OR_FAIL(hipMemcpyAsync(bgra_out, s->bgra_tmp.p, 4 * npix, hipMemcpyDeviceToHost, st));
-    unsigned long long cnt[16] = {0};
+    unsigned long long cnt[32] = {0};
     HIP_OR_FAIL(hipMemcpyAsync(cnt, s->counters.p, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
     if (cnt[4] != 0) return fail(TPT_ERR_HIP, "traversal stack overflow (BVH deeper than sized)");
@@ -585,9 +593,9 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
             std::fclose(f);
         }
     }
-    if (std::getenv("TPT_DEBUG_COUNTERS")) {   // raw kernel counters (phase-profiling builds fill 6..8)
+    if (std::getenv("TPT_DEBUG_COUNTERS")) {   // raw kernel counters (TPT_PROFILE_PHASES builds: 6..15 phases, 16..22 shading-pass sections)
         std::fprintf(stderr, "tpt counters:");
-        for (int i = 0; i < 16; ++i) std::fprintf(stderr, " %llu", cnt[i]);
+        for (int i = 0; i < 32; ++i) std::fprintf(stderr, " %llu", cnt[i]);
         std::fprintf(stderr, "\n");
     }
     if (stats) {

@@ -36,6 +36,9 @@
 #include "../common/tpt_math.hpp"
 #include "tpt.h"
 
+#ifndef TPT_PROBE_SHORTCUT
+#define TPT_PROBE_SHORTCUT 1   // no emissive triangle: resolve direct probes in the shading pass
+#endif
 #ifndef TPT_LEAF_KB
 #define TPT_LEAF_KB 8     // run the triangle branch once this many lanes are blocked ...
 #endif
@@ -655,7 +658,30 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
 #ifdef TPT_PROFILE_PHASES
     const unsigned long long t_wave0 = wall_clock64();
     unsigned long long p_done = 0, p_trav = 0, p_steps = 0, t_iter0 = 0, t_loop0 = 0, p_outer = 0;
-    unsigned long long p_sub[3] = {0, 0, 0};
+    // shading-pass sections (profiling builds only): every boundary drains
+    // the wave's outstanding memory operations, so a section is charged the
+    // latency of its own loads; the pass's first active lane adds the time
+    unsigned int p_sec[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t_sec = 0;
+    bool p_lead = false;
+#endif
+#ifdef TPT_PROFILE_PHASES
+#define TPT_SEC_BEGIN()                                                       \
+    {                                                                         \
+        __builtin_amdgcn_s_waitcnt(0);                                        \
+        t_sec = wall_clock64();                                               \
+        p_lead = __builtin_amdgcn_readfirstlane(lane) == lane;                \
+    }
+#define TPT_SEC(k)                                                            \
+    {                                                                         \
+        __builtin_amdgcn_s_waitcnt(0);                                        \
+        const unsigned long long t_ = wall_clock64();                         \
+        if (p_lead) p_sec[k] += (unsigned int)(t_ - t_sec);                   \
+        t_sec = t_;                                                           \
+    }
+#else
+#define TPT_SEC_BEGIN()
+#define TPT_SEC(k)
 #endif
     for (;;) {
 #ifdef TPT_PROFILE_PHASES
@@ -675,6 +701,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             ts = TS_TRAV;
         }
         if (ts == TS_DONE) {
+            TPT_SEC_BEGIN()
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
             V3 L = v3(0.0f, 0.0f, 0.0f);
@@ -725,6 +752,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 rec.put_dst(depth, mk, pm, dl);
                 after = true;
             }
+            TPT_SEC(1)
             V3 td = rd;
             bool shadow = false;
             if (lights_next) {
@@ -749,13 +777,23 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
                         float af2;
                         new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
-                        phase = PH_PROBE;
+                        if (TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) {
+                            // no triangle emits: the probe's emitter pass ends at the
+                            // root with no hit, exactly as a traversal would (the ray
+                            // is still counted: the reference traces it)
+                            ++c_trav;
+                            rec.put_dst(depth, mk, kNoProbe, direct);
+                            after = true;
+                        } else {
+                            phase = PH_PROBE;
+                        }
                     } else {
                         rec.put_dst(depth, mk, kNoProbe, direct);
                         after = true;
                     }
                 }
             }
+            TPT_SEC(2)
             if (after) {
                 const float e = MT(2 * (mk & 0x3fffffffu)).w;
                 if (e > 0.0f) {   // an emitter ends the path (:408-412); the unwind starts from e
@@ -769,10 +807,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     else phase = PH_EXT;
                 }
             }
-#ifdef TPT_PROFILE_PHASES
-            unsigned long long t_a = wall_clock64();
-            p_sub[0] += t_a - t_iter0;
-#endif
+            TPT_SEC(3)
             if (finish) {   // unwind (:416-431): levels depth-1 .. 0
                 for (int k = depth - 1; k >= 0; --k) {
                     const float af = rec.get(k, 0);
@@ -797,13 +832,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 total = total + L;
                 phase = PH_CAMERA;
             }
-#ifdef TPT_PROFILE_PHASES
-            {
-                const unsigned long long t_b = wall_clock64();
-                p_sub[1] += t_b - t_a;
-                t_a = t_b;
-            }
-#endif
+            TPT_SEC(4)
             V3 to = r.o;
             if (phase == PH_CAMERA) {
                 if (remaining == 0) {
@@ -829,18 +858,14 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     phase = PH_EXT;
                 }
             }
-#ifdef TPT_PROFILE_PHASES
-            {
-                const unsigned long long t_b = wall_clock64();
-                p_sub[2] += t_b - t_a;
-            }
-#endif
+            TPT_SEC(5)
             if (ts != TS_DEAD) {
                 ++c_trav;
                 trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
                            a.boxes_finite != 0);
                 ts = TS_TRAV;
             }
+            TPT_SEC(6)
         }
         if (__ballot(ts != TS_DEAD) == 0ull) break;
 #ifdef TPT_PROFILE_PHASES
@@ -930,6 +955,15 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         m_trav = o2 > m_trav ? o2 : m_trav;
     }
 #endif
+#ifdef TPT_PROFILE_PHASES
+    unsigned long long s_sec[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) s_sec[k] = wave_sum(p_sec[k]);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) atomicAdd(&a.counters[16 + k], s_sec[k]);
+    }
+#endif
     if (lane == 0) {
         atomicAdd(&a.counters[0], s_trav);
         atomicAdd(&a.counters[1], s_inner);
@@ -941,9 +975,6 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[6], p_done);
         atomicAdd(&a.counters[7], p_trav);
         atomicAdd(&a.counters[8], p_steps);
-        atomicAdd(&a.counters[9], p_sub[0]);
-        atomicAdd(&a.counters[10], p_sub[1]);
-        atomicAdd(&a.counters[11], p_sub[2]);
         atomicAdd(&a.counters[12], p_outer);
         const unsigned long long life = wall_clock64() - t_wave0;
         atomicMax(&a.counters[13], life);
