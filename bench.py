@@ -7,10 +7,15 @@ Workload (BASELINE.json configs[1]): input box.gltf (Cornell box), 1920x1080,
 copyToFB, inputs resident in HBM.  A "ray" is one traverseBVH call (primary,
 extension, direct probe, shadow), counted by the kernel.
 
-N GPUs: one process per GPU (torch.distributed.run), the frame is split in
-interleaved 16-row bands, each rank renders its band, one gather (RCCL) brings
-the bands to rank 0 inside the timed region.  Strong scaling (the frame is
-fixed).  value = rays of the whole frame / max-over-ranks step time.
+N GPUs: one process per GPU (torch.distributed.run).  Default (--scaling
+weak): a step is a batch of N frames of the workload above (seeds 42 .. 42+N-1;
+the reference re-seeds every frame, path_tracer.cu:493,513), each frame split
+across all N GPUs in interleaved 16-row bands, so every GPU renders the pixel
+mix of one whole frame in one launch; one all-to-all (RCCL over xGMI) leaves
+frame f on rank f inside the timed region.  --scaling strong: one frame split
+across the N GPUs, one gather to rank 0 (bounded by the heaviest pixels'
+serial sample chains).  value = rays of all frames /
+max-over-ranks step time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -47,6 +52,9 @@ def parse():
                     help="gloo: rehearse the N-rank path on one GPU (all ranks on device 0, gather via host)")
     ap.add_argument("--verify-gather", action="store_true",
                     help="rank 0 re-renders the whole frame alone and checks the gathered frame bit for bit")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: N frames per step, each banded across the N ranks (all-to-all); "
+                         "strong: one frame banded across the N ranks (gather)")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of an N-rank run: render only rank 0's bands of an N-way split")
     ap.add_argument("--env", choices=["sky", "none"], default=None, help="procedural equirect env on miss")
@@ -183,19 +191,27 @@ def main():
         args.env = None
     if args.env == "sky":
         pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), device=dev)
-    radiance = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
     band = (args.band_rows, world, rank)
+    ranks = world
     if args.emulate_ranks > 1 and world == 1:
-        band = (args.band_rows, args.emulate_ranks, 0)
+        ranks = args.emulate_ranks
+        band = (args.band_rows, ranks, 0)
+    # weak scaling: a batch of `ranks` frames, frame f with seed + f, each banded across all ranks
+    n_frames = ranks if args.scaling == "weak" else 1
+    seeds = [args.seed + f for f in range(n_frames)]
+    radiances = [torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}") for _ in range(n_frames)]
+    flags = args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0)
 
     def step():
-        st = pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,
-                        radiance=radiance, band=band, spp_per_launch=args.spp_per_launch,
-                        flags=args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0), refill=args.refill)
+        st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
+                              radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
+                              refill=args.refill)
         if world == 1:
-            return st, radiance
-        src = radiance if args.dist_backend == "nccl" else radiance.cpu()   # gloo gathers host tensors
-        return st, shard.gather_frame(src, H, args.band_rows, world, rank)
+            return st, radiances[0]
+        src = radiances if args.dist_backend == "nccl" else [r.cpu() for r in radiances]   # gloo: host tensors
+        if args.scaling == "weak":
+            return st, shard.exchange_frames(src, H, args.band_rows, world, rank)
+        return st, shard.gather_frame(src[0], H, args.band_rows, world, rank)
 
     for _ in range(args.warmup):
         step()
@@ -232,6 +248,23 @@ def main():
         tot["trace_ms_max"] = tot["trace_ms"]
         tot["trace_launches_max"] = tot["trace_launches"]
 
+    def verify(frame):
+        """This rank's assembled frame (weak: frame `rank`, seed + rank; strong:
+        rank 0's whole frame) against one GPU rendering every row of it."""
+        full = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
+        sd = args.seed + (rank if args.scaling == "weak" else 0)
+        pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=sd, max_depth=args.depth,
+                   radiance=full, band=(args.band_rows, 1, 0), flags=flags, refill=args.refill)
+        got = frame.to(full.device).contiguous()
+        return bool(torch.equal(got.view(torch.int32), full.view(torch.int32)))
+
+    verified = None
+    if world > 1 and args.verify_gather and args.scaling == "weak":
+        ok = torch.tensor([1.0 if verify(frame) else 0.0], dtype=torch.float64,
+                          device=f"cuda:{dev}" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        verified = bool(ok.item() == 1.0)
+
     if rank == 0:
         K = args.steps
         rays = tot["traversals"]
@@ -245,13 +278,17 @@ def main():
         avg_launch_s = (l_tot["trace_ms"] / nl) / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
+        batch = (f" x {n_frames} frames (seeds {seeds[0]}..{seeds[-1]}), each banded across {ranks} ranks"
+                 if n_frames > 1 else "")
         config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}"
-                              + (" env sky" if args.env else "") + (" env-IS" if args.env_is else ""),
+                              + (" env sky" if args.env else "") + (" env-IS" if args.env_is else "") + batch,
                   "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
                   "max_depth": args.depth, "seed": args.seed,
+                  "frames_per_step": n_frames,
                   "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + "
-                                 + ("RCCL gather" if args.dist_backend == "nccl" else "gloo gather (1-GPU rehearsal)")
-                  if world > 1 else "1 GPU"}
+                                 + ("RCCL " if args.dist_backend == "nccl" else "gloo (1-GPU rehearsal) ")
+                                 + ("all-to-all" if args.scaling == "weak" else "gather")
+                  if world > 1 else ("1 GPU" if ranks == 1 else f"1 GPU, rank 0 of {ranks} emulated")}
         if os.path.exists(args.pmc_json):
             try:
                 with open(args.pmc_json) as f:
@@ -271,7 +308,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": data_note(args),
@@ -290,13 +327,9 @@ def main():
                                    "bvh_build_once": round(build_ms, 3)},
         }
         if world > 1 and args.verify_gather:
-            # the assembled frame must equal one GPU rendering every row (the RNG
-            # subsequence is the global pixel index, path_tracer.cu:39,320)
-            full = torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}")
-            pt.doTrace(d_scene, scene.m_camera, None, args.spp, seed=args.seed, max_depth=args.depth,
-                       radiance=full, band=(args.band_rows, 1, 0), refill=args.refill)
-            got = frame.to(full.device).contiguous()
-            out["gather_verified"] = bool(torch.equal(got.view(torch.int32), full.view(torch.int32)))
+            # the assembled frame(s) must equal one GPU rendering every row (the
+            # RNG subsequence is the global pixel index, path_tracer.cu:39,320)
+            out["gather_verified"] = verified if args.scaling == "weak" else verify(frame)
         if world == 1 and args.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

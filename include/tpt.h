@@ -152,6 +152,17 @@ tpt_status tpt_render(tpt_scene* scene, const tpt_env* env, const tpt_camera* ca
                       const tpt_params* params, float* radiance_out, uint8_t* bgra_out,
                       tpt_stats* stats);
 
+/* A batch of independent frames in one trace launch: frame f is a doTrace
+ * with seed seeds[f] (the reference re-seeds every frame from time(),
+ * path_tracer.cu:493-494,513); all frames share params (size, spp, bands,
+ * flags) and params->seed is ignored.  Frame f is bit-identical to
+ * tpt_render with seed seeds[f].  Used to keep every GPU of a node busy on
+ * its share of several frames at once (bench.py weak scaling).
+ *   radiance_outs / bgra_outs: nullable arrays of n_frames nullable pointers,
+ *   each as in tpt_render.  stats: summed over the batch. */
+tpt_status tpt_render_frames(tpt_scene* scene, const tpt_env* env, const tpt_camera* camera,
+                             const tpt_params* params, int32_t n_frames, const uint64_t* seeds,
+                             float* const* radiance_outs, uint8_t* const* bgra_outs, tpt_stats* stats);
 /* Introspection for tests: copy back the built BVH in the reference node
  * layout (bvh.cuh:52-58, 36 B/node, 2F-1 nodes) and the sorted Morton keys. */
 tpt_status tpt_scene_read_bvh(tpt_scene* scene, void* nodes36, int64_t* keys);

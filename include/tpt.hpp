@@ -173,6 +173,30 @@ public:
         return st;
     }
 
+    // A batch of independent frames (seeds[f]) in one trace launch
+    // (tpt_render_frames); frame f equals doTrace with seed seeds[f].
+    tpt_stats doTraceFrames(DeviceScene& scene, const Camera& camera, const std::vector<uint64_t>& seeds,
+                            const std::vector<uint8_t*>& framebuffers, int nSamplesPerPixel, int max_depth = 8,
+                            const std::vector<float*>& radiances = {}, int band_count = 1, int band_index = 0) {
+        if (!scene.built()) scene.build();
+        const size_t n = seeds.size();
+        if ((!framebuffers.empty() && framebuffers.size() != n) || (!radiances.empty() && radiances.size() != n))
+            throw std::runtime_error("doTraceFrames: need one output buffer per frame");
+        tpt_params p{};
+        p.width = m_width;
+        p.height = m_height;
+        p.spp = nSamplesPerPixel;
+        p.max_depth = max_depth;
+        p.band_rows = 16;
+        p.band_count = band_count;
+        p.band_index = band_index;
+        tpt_stats st{};
+        check(tpt_render_frames(scene.handle(), envLight.handle(), &camera.c, &p, (int32_t)n, seeds.data(),
+                                radiances.empty() ? nullptr : radiances.data(),
+                                framebuffers.empty() ? nullptr : framebuffers.data(), &st));
+        return st;
+    }
+
     // render(meshFile) (path_tracer.cu:556-579), headless: the reference loops
     // frames in a window; this renders `frames` frames and returns the last --
     // with progressive = true each frame adds its samples to the previous ones.

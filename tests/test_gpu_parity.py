@@ -218,6 +218,45 @@ def test_band_sharding_bit_identical(built):
         assert np.array_equal(_bits(acc), _bits(full)), count
 
 
+def test_frame_batch_bit_identical(built):
+    """tpt_render_frames: a batch of frames in one launch (grid z), each equal
+    bit for bit to a separate doTrace with its seed -- whole frames, banded
+    frames (the weak-scaling split), host and torch device outputs, bgra too;
+    a progressive continuation of the batch equals one call with the total spp."""
+    import torch
+    s, d, _ = built["box"]
+    W, H, spp = 48, 40, 6
+    seeds = [42, 43, 7]
+    pt = T.PathTracer("", W, H, 0)
+    singles, fbs = [], []
+    for sd in seeds:
+        r = np.zeros((H, W, 3), np.float32)
+        fb = np.zeros((H, W, 4), np.uint8)
+        pt.doTrace(d, s.m_camera, fb, spp, seed=sd, radiance=r)
+        singles.append(r)
+        fbs.append(fb)
+    rads = [np.zeros((H, W, 3), np.float32) for _ in seeds]
+    fbo = [np.zeros((H, W, 4), np.uint8) for _ in seeds]
+    st = pt.doTraceFrames(d, s.m_camera, seeds, fbo, spp, radiances=rads)
+    assert st["trace_launches"] == 1 and st["pixels"] == W * H * len(seeds)
+    for f in range(len(seeds)):
+        assert np.array_equal(_bits(rads[f]), _bits(singles[f])), f
+        assert np.array_equal(fbo[f], fbs[f]), f
+    # banded: every rank renders its rows of every frame (bench.py weak scaling)
+    dev = [torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0") for _ in seeds]
+    for idx in range(3):
+        pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=dev, band=(16, 3, idx))
+    for f in range(len(seeds)):
+        assert np.array_equal(_bits(dev[f].cpu().numpy()), _bits(singles[f])), f
+    # progressive continuation of the whole batch
+    prog = [np.zeros((H, W, 3), np.float32) for _ in seeds]
+    pt.doTraceFrames(d, s.m_camera, seeds, None, 2, radiances=prog)
+    st = pt.doTraceFrames(d, s.m_camera, seeds, None, 4, radiances=prog, accumulate=True)
+    assert st["accumulated_spp"] == spp
+    for f in range(len(seeds)):
+        assert np.array_equal(_bits(prog[f]), _bits(singles[f])), f
+
+
 def test_spp_chunking_bit_identical(built):
     s, d, _ = built["box2"]
     W, H, spp = 32, 32, 12

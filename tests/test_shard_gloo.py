@@ -60,3 +60,35 @@ def test_band_rows_partition():
         assert sorted(rows.tolist()) == list(range(1080))
         hs = [len(shard.band_row_ids(1080, 16, world, r)) for r in range(world)]
         assert max(hs) - min(hs) <= 16
+
+
+def _worker_frames(rank, world, port, out_dir):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from tinypathtracer_amd import shard
+    ps = O.load_scene(os.path.join(ROOT, "tests", "golden", "scenes", "box.gltf"))
+    # weak scaling: this rank's bands of every frame of the batch (frame f: seed 42 + f)
+    rads = [torch.from_numpy(O.render(ps, W, H, SPP, 8, 42 + f, trig_mode=1, band_rows=BAND, band_count=world,
+                                      band_index=rank, threads=1)[0]) for f in range(world)]
+    frame = shard.exchange_frames(rads, H, BAND, world, rank)
+    np.save(os.path.join(out_dir, f"frame{rank}.npy"), frame.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_frame_batch_all_to_all(tmp_path, world):
+    """Frame batch across ranks (bench.py weak scaling): after the all-to-all,
+    rank f holds frame f (seed 42 + f) bit-identical to a one-process render."""
+    mp.start_processes(_worker_frames, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    ps = O.load_scene(os.path.join(ROOT, "tests", "golden", "scenes", "box.gltf"))
+    for f in range(world):
+        full, _, _ = O.render(ps, W, H, SPP, 8, 42 + f, trig_mode=1)
+        got = np.load(str(tmp_path / f"frame{f}.npy"))
+        assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), f

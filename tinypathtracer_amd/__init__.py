@@ -309,6 +309,41 @@ class PathTracer:
         check(lib().tpt_render(d_scene.handle, env, C.byref(cam), C.byref(p), rad_p, fb_p, C.byref(st)))
         return st.as_dict()
 
+    def doTraceFrames(self, d_scene: DeviceScene, camera: Camera, seeds, framebuffers=None,
+                      nSamplesPerPixel: int = 64, max_depth: int = 8, radiances=None, band=(16, 1, 0),
+                      spp_per_launch: int = 0, flags: int = 0, refill: int = 0, accumulate: bool = False):
+        """A batch of independent frames in one trace launch (tpt_render_frames):
+        frame f is doTrace(..., seed=seeds[f]) bit for bit.  framebuffers /
+        radiances: None or one buffer (or None) per frame."""
+        if not d_scene.built:
+            d_scene.build()
+        seeds = [int(x) for x in seeds]
+        n = len(seeds)
+        if n == 0:
+            raise ValueError("no frames")
+        if accumulate:
+            flags |= _lib.FLAG_ACCUMULATE
+        W, H = self.m_width, self.m_height
+        p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seeds[0], band[0], band[1], band[2], spp_per_launch,
+                        flags, refill)
+        st = _lib.Stats()
+        env = self.envLight.handle if self.envLight is not None else None
+
+        def ptrs(bufs):
+            if bufs is None:
+                return None
+            if len(bufs) != n:
+                raise ValueError("need one output buffer per frame")
+            arr = (C.c_void_p * n)(*[(_addr(b).value if b is not None else None) for b in bufs])
+            return C.cast(arr, C.POINTER(C.c_void_p)), arr
+
+        rp, fp = ptrs(radiances), ptrs(framebuffers)
+        cs = (C.c_uint64 * n)(*seeds)
+        cam = camera.to_c()
+        check(lib().tpt_render_frames(d_scene.handle, env, C.byref(cam), C.byref(p), n, cs,
+                                      rp[0] if rp else None, fp[0] if fp else None, C.byref(st)))
+        return st.as_dict()
+
     def render(self, meshFile: str, nSamplesPerPixel: int = 64, seed=None, max_depth: int = 8, frames: int = 1):
         scene = Scene(meshFile, "gltf")
         d_scene = scene.copySceneToDevice(self.device).build()

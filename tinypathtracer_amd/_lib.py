@@ -81,6 +81,9 @@ SIGNATURES = [
     ("tpt_env_destroy", None, [C.c_void_p]),
     ("tpt_render", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_void_p,
                              C.c_void_p, C.POINTER(Stats)]),
+    ("tpt_render_frames", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_int32,
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                    C.POINTER(Stats)]),
     ("tpt_scene_read_bvh", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_scene_read_world", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_debug_rng_init", C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]),

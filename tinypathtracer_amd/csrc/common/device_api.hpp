@@ -70,6 +70,7 @@ struct TraceArgs {
     // frame
     int32_t width, height;
     int32_t band_rows, band_count, band_index, band_height;   // band_height: rows in this band
+    int32_t n_frames;                    // frames of the batch (grid z); frame f's state at f * planes * W*H
     int32_t max_depth;
     int32_t samples;                     // samples for this launch
     int32_t flags;

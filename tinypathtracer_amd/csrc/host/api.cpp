@@ -190,7 +190,8 @@ struct tpt_scene {
     // progressive accumulation (TPT_FLAG_ACCUMULATE): the frame the rng/accum state belongs to
     bool acc_valid = false;
     int acc_w = 0, acc_h = 0, acc_rows = 0, acc_count = 0, acc_index = 0;
-    uint64_t acc_seed = 0, acc_spp = 0;
+    uint64_t acc_spp = 0;
+    std::vector<uint64_t> acc_seeds;        // one per frame of the batch
 
     ~tpt_scene() {
         DeviceGuard g(device);
@@ -457,8 +458,17 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
 
 tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, const tpt_params* p,
                       float* radiance_out, uint8_t* bgra_out, tpt_stats* stats) {
+    if (!p) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    const uint64_t seed = p->seed;
+    return tpt_render_frames(s, env, cam, p, 1, &seed, &radiance_out, &bgra_out, stats);
+}
+
+tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, const tpt_params* p,
+                             int32_t n_frames, const uint64_t* seeds, float* const* radiance_outs,
+                             uint8_t* const* bgra_outs, tpt_stats* stats) {
     auto t_start = std::chrono::steady_clock::now();
-    if (!s || !cam || !p) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    if (!s || !cam || !p || !seeds) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    if (n_frames < 1 || n_frames > 65535) return fail(TPT_ERR_INVALID_ARG, "bad frame count");
     if (!s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built (call tpt_scene_build)");
     if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 1 || p->max_depth > 64)
         return fail(TPT_ERR_INVALID_ARG, "bad frame parameters");
@@ -471,23 +481,27 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     hipStream_t st = s->stream;
     const int W = p->width, H = p->height;
     const size_t npix = (size_t)W * (size_t)H;
+    const size_t nf = (size_t)n_frames;
     const int bh = band_height_of(H, band_rows, band_count, p->band_index);
+    const std::vector<uint64_t> fseeds(seeds, seeds + nf);
 
     const bool resume = (p->flags & TPT_FLAG_ACCUMULATE) && s->acc_valid && s->acc_w == W && s->acc_h == H &&
                         s->acc_rows == band_rows && s->acc_count == band_count && s->acc_index == p->band_index &&
-                        s->acc_seed == p->seed && s->rng.n == 6 * npix && s->accum.n == 3 * npix;
+                        s->acc_seeds == fseeds && s->rng.n == 6 * npix * nf && s->accum.n == 3 * npix * nf;
     s->acc_valid = false;   // re-armed once this call has completed
-    HIP_OR_FAIL(s->rng.alloc(6 * npix));
-    HIP_OR_FAIL(s->accum.alloc(3 * npix));
+    // per-frame state planes, frame f at offset f * (6|3) * npix
+    HIP_OR_FAIL(s->rng.alloc(6 * npix * nf));
+    HIP_OR_FAIL(s->accum.alloc(3 * npix * nf));
     HIP_OR_FAIL(s->counters.alloc(32));
-    if (!resume) HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * sizeof(float), st));   // thrust::fill (:534)
+    if (!resume) HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * nf * sizeof(float), st));   // thrust::fill (:534)
     HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 32 * sizeof(unsigned long long), st));
 
-    // setupRandSeed (:513); a progressive call continues the persisted streams
+    // setupRandSeed (:513), one seed per frame; a progressive call continues the persisted streams
     HIP_OR_FAIL(hipEventRecord(s->ev[0], st));
     if (bh > 0 && !resume)
-        HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, p->seed, W, band_rows, band_count, p->band_index, bh, H,
-                                         s->rng.p, st));
+        for (size_t f = 0; f < nf; ++f)
+            HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, fseeds[f], W, band_rows, band_count, p->band_index, bh, H,
+                                             s->rng.p + f * 6 * npix, st));
     HIP_OR_FAIL(hipEventRecord(s->ev[1], st));
     const uint64_t total_spp = (resume ? s->acc_spp : 0) + (uint64_t)p->spp;
     if (total_spp > (uint64_t)INT32_MAX) return fail(TPT_ERR_INVALID_ARG, "accumulated spp overflow");
@@ -502,6 +516,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     a.band_count = band_count;
     a.band_index = p->band_index;
     a.band_height = bh;
+    a.n_frames = n_frames;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
     // A15 env next-event estimation: opt-in, needs an env with a non-empty distribution
@@ -512,7 +527,8 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     a.counters = s->counters.p;
     a.debug_waves = nullptr;
     const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");   // phase-profiling builds only
-    const size_t dbg_words = 8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 15) / 16);
+    const size_t dbg_words =
+        8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 15) / 16) * nf;
     if (dbg_path) {
         HIP_OR_FAIL(s->debug.alloc(dbg_words));
         HIP_OR_FAIL(hipMemsetAsync(s->debug.p, 0, dbg_words * sizeof(unsigned long long), st));
@@ -521,10 +537,10 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
 
     int chunk = p->spp_per_launch;
     if (chunk <= 0) {
-        // One launch per frame: every launch ends in a tail where CUs drain
-        // (measured ~7 ms per launch on box 1080p, 9% at 64-spp chunks).
-        // Chunk only past ~4096 spp at 1080p so one launch stays below ~5 s.
-        const double band_pix = (double)W * (double)std::max(bh, 1);
+        // One launch per frame batch: every launch ends in a tail where CUs
+        // drain (measured ~7 ms per launch on box 1080p, 9% at 64-spp chunks).
+        // Chunk only past ~4096 spp of 1080p pixels so one launch stays below ~5 s.
+        const double band_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
         chunk = (int)std::max(1.0, std::floor(4096.0 * 2073600.0 / band_pix));
     }
     chunk = std::min(chunk, p->spp);
@@ -542,45 +558,50 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
         ++launches;
     }
 
-    // copyToFB (:553) + radiance readout
-    const bool rad_dev = is_device_ptr(radiance_out);
-    const bool bgra_dev = is_device_ptr(bgra_out);
-    tpt::ResolveArgs r{};
-    r.accum = s->accum.p;
-    r.width = W;
-    r.height = H;
-    r.band_rows = band_rows;
-    r.band_count = band_count;
-    r.band_index = p->band_index;
-    r.band_height = bh;
-    r.spp = (int)total_spp;
-    if (radiance_out) {
-        if (rad_dev) {
-            r.radiance = radiance_out;
-        } else {
-            HIP_OR_FAIL(s->radiance_tmp.alloc(3 * npix));
-            HIP_OR_FAIL(hipMemcpyAsync(s->radiance_tmp.p, radiance_out, 3 * npix * sizeof(float),
-                                       hipMemcpyHostToDevice, st));
-            r.radiance = s->radiance_tmp.p;
-        }
-    }
-    if (bgra_out) {
-        if (bgra_dev) {
-            r.bgra = bgra_out;
-        } else {
-            HIP_OR_FAIL(s->bgra_tmp.alloc(4 * npix));
-            HIP_OR_FAIL(hipMemcpyAsync(s->bgra_tmp.p, bgra_out, 4 * npix, hipMemcpyHostToDevice, st));
-            r.bgra = s->bgra_tmp.p;
-        }
-    }
+    // copyToFB (:553) + radiance readout, per frame
     HIP_OR_FAIL(hipEventRecord(s->ev[2], st));
-    if (bh > 0 && (r.radiance || r.bgra)) HIP_OR_FAIL(tpt::launch_resolve(r, st));
+    for (size_t f = 0; f < nf; ++f) {
+        float* radiance_out = radiance_outs ? radiance_outs[f] : nullptr;
+        uint8_t* bgra_out = bgra_outs ? bgra_outs[f] : nullptr;
+        const bool rad_dev = is_device_ptr(radiance_out);
+        const bool bgra_dev = is_device_ptr(bgra_out);
+        tpt::ResolveArgs r{};
+        r.accum = s->accum.p + f * 3 * npix;
+        r.width = W;
+        r.height = H;
+        r.band_rows = band_rows;
+        r.band_count = band_count;
+        r.band_index = p->band_index;
+        r.band_height = bh;
+        r.spp = (int)total_spp;
+        if (radiance_out) {
+            if (rad_dev) {
+                r.radiance = radiance_out;
+            } else {
+                HIP_OR_FAIL(s->radiance_tmp.alloc(3 * npix));
+                HIP_OR_FAIL(hipMemcpyAsync(s->radiance_tmp.p, radiance_out, 3 * npix * sizeof(float),
+                                           hipMemcpyHostToDevice, st));
+                r.radiance = s->radiance_tmp.p;
+            }
+        }
+        if (bgra_out) {
+            if (bgra_dev) {
+                r.bgra = bgra_out;
+            } else {
+                HIP_OR_FAIL(s->bgra_tmp.alloc(4 * npix));
+                HIP_OR_FAIL(hipMemcpyAsync(s->bgra_tmp.p, bgra_out, 4 * npix, hipMemcpyHostToDevice, st));
+                r.bgra = s->bgra_tmp.p;
+            }
+        }
+        if (bh > 0 && (r.radiance || r.bgra)) HIP_OR_FAIL(tpt::launch_resolve(r, st));
+        // host outputs share one staging buffer: copy back before the next frame reuses it
+        if (radiance_out && !rad_dev)
+            HIP_OR_FAIL(hipMemcpyAsync(radiance_out, s->radiance_tmp.p, 3 * npix * sizeof(float),
+                                       hipMemcpyDeviceToHost, st));
+        if (bgra_out && !bgra_dev)
+            HIP_OR_FAIL(hipMemcpyAsync(bgra_out, s->bgra_tmp.p, 4 * npix, hipMemcpyDeviceToHost, st));
+    }
     HIP_OR_FAIL(hipEventRecord(s->ev[3], st));
-    if (radiance_out && !rad_dev)
-        HIP_OR_FAIL(hipMemcpyAsync(radiance_out, s->radiance_tmp.p, 3 * npix * sizeof(float), hipMemcpyDeviceToHost,
-                                   st));
-    if (bgra_out && !bgra_dev)
-        HIP_OR_FAIL(hipMemcpyAsync(bgra_out, s->bgra_tmp.p, 4 * npix, hipMemcpyDeviceToHost, st));
     unsigned long long cnt[32] = {0};
     HIP_OR_FAIL(hipMemcpyAsync(cnt, s->counters.p, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
@@ -606,7 +627,7 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
         stats->accumulated_spp = total_spp;
         stats->leaf_tests = cnt[2];
         stats->shade_hits = cnt[3];
-        stats->pixels = (uint64_t)W * (uint64_t)bh;
+        stats->pixels = (uint64_t)W * (uint64_t)bh * (uint64_t)nf;
         stats->samples = stats->pixels * (uint64_t)p->spp;
         float ms = 0.0f;
         (void)hipEventElapsedTime(&ms, s->ev[0], s->ev[1]);
@@ -618,15 +639,15 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
         stats->total_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
-    // the persisted streams and sums now belong to this frame: a following
-    // TPT_FLAG_ACCUMULATE call with the same frame continues them
+    // the persisted streams and sums now belong to this batch: a following
+    // TPT_FLAG_ACCUMULATE call with the same frames continues them
     s->acc_valid = true;
     s->acc_w = W;
     s->acc_h = H;
     s->acc_rows = band_rows;
     s->acc_count = band_count;
     s->acc_index = p->band_index;
-    s->acc_seed = p->seed;
+    s->acc_seeds = fseeds;
     s->acc_spp = total_spp;
     return TPT_OK;
 }

@@ -595,6 +595,9 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
+    // frame batch: frame blockIdx.z owns its own RNG and accumulator planes
+    uint32_t* const g_rng = a.rng + (size_t)blockIdx.z * 6 * npix;
+    float* const g_acc = a.accum + (size_t)blockIdx.z * 3 * npix;
     const int nint = a.n_faces - 1;
     // Material table in LDS when small (every shading, probe and unwind step
     // reads it; LDS latency instead of a dependent global load).  The copy is
@@ -640,8 +643,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     V3 total = v3(0.0f, 0.0f, 0.0f);
     if (active) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) st[i] = a.rng[i * npix + off];
-        total = v3(a.accum[off], a.accum[npix + off], a.accum[2 * npix + off]);
+        for (int i = 0; i < 6; ++i) st[i] = g_rng[i * npix + off];
+        total = v3(g_acc[off], g_acc[npix + off], g_acc[2 * npix + off]);
     }
     int remaining = a.samples;
     int phase = PH_CAMERA;
@@ -939,10 +942,10 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     }
     if (active) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) a.rng[i * npix + off] = st[i];
-        a.accum[off] = total.x;
-        a.accum[npix + off] = total.y;
-        a.accum[2 * npix + off] = total.z;
+        for (int i = 0; i < 6; ++i) g_rng[i * npix + off] = st[i];
+        g_acc[off] = total.x;
+        g_acc[npix + off] = total.y;
+        g_acc[2 * npix + off] = total.z;
     }
     const unsigned long long s_wide = wave_sum(c_wide);
     const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
@@ -981,7 +984,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[14], life);
         atomicAdd(&a.counters[15], 1ull);
         if (a.debug_waves) {   // per-wave record: start, life, steps, shading passes, rays, wide, max lane rays, done-time
-            const unsigned long long wid = ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
+            const unsigned long long wid =
+                ((((unsigned long long)blockIdx.z * gridDim.y) + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave;
             unsigned long long* o = a.debug_waves + 8 * wid;
             o[0] = t_wave0;
             o[1] = life;
@@ -1092,7 +1096,7 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
-    dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16);
+    dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16, a.n_frames > 0 ? a.n_frames : 1);
     if (a.flags & TPT_FLAG_REF_ORDER) {
         // the reference's visit order (tests, diagnostics): one general variant
         const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, false);
