@@ -484,6 +484,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     const size_t nf = (size_t)n_frames;
     const int bh = band_height_of(H, band_rows, band_count, p->band_index);
     const std::vector<uint64_t> fseeds(seeds, seeds + nf);
+    // the trace grid's y extent is (band row blocks) x frames
+    if ((size_t)((bh + 15) / 16) * nf > 65535) return fail(TPT_ERR_INVALID_ARG, "frame batch too large for one launch");
 
     const bool resume = (p->flags & TPT_FLAG_ACCUMULATE) && s->acc_valid && s->acc_w == W && s->acc_h == H &&
                         s->acc_rows == band_rows && s->acc_count == band_count && s->acc_index == p->band_index &&

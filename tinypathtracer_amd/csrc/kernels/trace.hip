@@ -588,16 +588,21 @@ template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bo
 __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // grid y interleaves the frames of a batch: consecutive workgroups render the
+    // same screen rows of successive frames, so the resident tiles keep the
+    // screen locality of a single frame (node reuse in L1/L2)
+    const int nfr = a.n_frames > 0 ? a.n_frames : 1;
+    const int frame = (int)blockIdx.y % nfr;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int ly = ((int)blockIdx.y / nfr) * 16 + (wave >> 1) * 8 + (lane >> 3);
     const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
     const bool active = x < a.width && ly < a.band_height && y < a.height;
     uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
-    // frame batch: frame blockIdx.z owns its own RNG and accumulator planes
-    uint32_t* const g_rng = a.rng + (size_t)blockIdx.z * 6 * npix;
-    float* const g_acc = a.accum + (size_t)blockIdx.z * 3 * npix;
+    // frame batch: each frame owns its own RNG and accumulator planes
+    uint32_t* const g_rng = a.rng + (size_t)frame * 6 * npix;
+    float* const g_acc = a.accum + (size_t)frame * 3 * npix;
     const int nint = a.n_faces - 1;
     // Material table in LDS when small (every shading, probe and unwind step
     // reads it; LDS latency instead of a dependent global load).  The copy is
@@ -985,7 +990,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[15], 1ull);
         if (a.debug_waves) {   // per-wave record: start, life, steps, shading passes, rays, wide, max lane rays, done-time
             const unsigned long long wid =
-                ((((unsigned long long)blockIdx.z * gridDim.y) + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wave;
+                ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
             unsigned long long* o = a.debug_waves + 8 * wid;
             o[0] = t_wave0;
             o[1] = life;
@@ -1096,7 +1101,7 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
-    dim3 grid((a.width + 15) / 16, (a.band_height + 15) / 16, a.n_frames > 0 ? a.n_frames : 1);
+    dim3 grid((a.width + 15) / 16, ((a.band_height + 15) / 16) * (a.n_frames > 0 ? a.n_frames : 1));
     if (a.flags & TPT_FLAG_REF_ORDER) {
         // the reference's visit order (tests, diagnostics): one general variant
         const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, false);
