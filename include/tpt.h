@@ -142,6 +142,18 @@ void tpt_scene_destroy(tpt_scene* scene);
 tpt_status tpt_env_create(const uint8_t* rgba, int32_t width, int32_t height, int device, tpt_env** out);
 void tpt_env_destroy(tpt_env* env);
 
+/* Env map from an image file: EnvLight(file) (include/env_light.cuh:8-18,
+ * src/texture.cu:64-171, include/picture.h:19-45).  Decodes JPEG (baseline and
+ * progressive Huffman, libjpeg's default islow IDCT / fancy upsampling / YCbCr
+ * tables) or binary PPM natively into the texel layout tpt_env_create takes
+ * (RGBA8, row 0 = bottom).  Errors: TPT_ERR_IO (cannot open), TPT_ERR_PARSE
+ * (unsupported or corrupt image, e.g. grayscale, which the reference's
+ * Texture also rejects). */
+tpt_status tpt_env_load(const char* path, int device, tpt_env** out);
+/* The decoder alone: *rgba is allocated by the library (free with
+ * tpt_image_free), width*height*4 bytes, row 0 = bottom. */
+tpt_status tpt_image_load(const char* path, uint8_t** rgba, int32_t* width, int32_t* height);
+void tpt_image_free(uint8_t* rgba);
 /* One frame == doTrace: setupRandSeed, trace (spp), copyToFB.
  *   radiance_out: nullable, width*height*3 floats = color/spp, row 0 = bottom;
  *                 host or device pointer (detected).  Only band rows written.

@@ -124,6 +124,13 @@ public:
         check(tpt_env_create(flipped.data(), width, height, device, &e));
         env_.reset(e, Free());
     }
+    // EnvLight(file) (env_light.cuh:8-18): JPEG or binary PPM decoded natively
+    // as FreeImage would (tpt_env_load); throws std::runtime_error like Picture.
+    explicit EnvLight(const std::string& file, int device = 0) {
+        tpt_env* e = nullptr;
+        check(tpt_env_load(file.c_str(), device, &e));
+        env_.reset(e, Free());
+    }
     const tpt_env* handle() const { return env_.get(); }
 
 private:

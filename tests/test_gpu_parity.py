@@ -356,3 +356,38 @@ def test_cpp_cli_matches_python_host(tmp_path, frames):
     T.PathTracer("", W, H, 0).doTrace(d, s.m_camera, None, spp, seed=42, radiance=rad)
     d.close()
     assert np.array_equal(pfm.view(np.uint32), rad.view(np.uint32))
+
+
+def test_env_from_jpeg_file(built, tmp_path):
+    """EnvLight(file) (env_light.cuh:8-18): a JPEG env decoded natively
+    (tpt_env_load, C++ CLI --env) renders bit-identically to the same texels
+    decoded by libjpeg (PIL) and uploaded as an array; the C++ CLI agrees."""
+    import subprocess
+    from PIL import Image
+    s, d, _ = built["ball"]
+    W, H, spp = 40, 24, 4
+    sky = T.procedural_sky(256, 128)[..., :3]
+    jpg = str(tmp_path / "sky.jpg")
+    Image.fromarray(sky).save(jpg, "JPEG", quality=85, progressive=True)
+    decoded = np.asarray(Image.open(jpg).convert("RGB"))
+    a = T.PathTracer("", W, H, 0)
+    a.envLight = T.EnvLight(jpg)                 # native decoder
+    assert a.envLight.rgba is None
+    b = T.PathTracer("", W, H, 0)
+    b.envLight = T.EnvLight(decoded)             # libjpeg's texels as an array
+    ra = np.zeros((H, W, 3), np.float32)
+    rb = np.zeros((H, W, 3), np.float32)
+    a.doTrace(d, s.m_camera, None, spp, seed=3, radiance=ra)
+    b.doTrace(d, s.m_camera, None, spp, seed=3, radiance=rb)
+    assert ra.max() > 0
+    assert np.array_equal(_bits(ra), _bits(rb))
+    exe = os.path.join(ROOT, "tinypathtracer_amd", "tpt_render")
+    out = str(tmp_path / "cli")
+    res = subprocess.run([exe, scene_path("ball"), "--width", str(W), "--height", str(H), "--spp", str(spp),
+                          "--seed", "3", "--env", jpg, "--out", out], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    with open(out + ".pfm", "rb") as f:
+        for _ in range(3):
+            f.readline()
+        pfm = np.frombuffer(f.read(), np.float32).reshape(H, W, 3)
+    assert np.array_equal(pfm.view(np.uint32), _bits(ra))

@@ -217,8 +217,10 @@ def procedural_sky(width=2048, height=1024):
 
 class EnvLight:
     """EnvLight (env_light.cuh:8-18): equirect radiance, used on miss (A14).
-    Accepts an image file (PIL-readable, PFM/PPM) or an RGBA/RGB array in image
-    order (row 0 = top); stored row 0 = bottom like FreeImage (picture.h:41-43)."""
+    Accepts an image file or an RGBA/RGB array in image order (row 0 = top);
+    stored row 0 = bottom like FreeImage (picture.h:41-43).  JPEG and binary
+    PPM files are decoded by the library's native decoder (tpt_env_load, the
+    FreeImage/libjpeg arithmetic); other formats go through PIL."""
 
     def __init__(self, source=None, device: int = 0):
         self.device = device
@@ -227,6 +229,10 @@ class EnvLight:
             self.rgba = None
             return
         if isinstance(source, str):
+            if self._native(source):
+                self.rgba = None
+                check(lib().tpt_env_load(source.encode(), device, C.byref(self.handle)))
+                return
             img = self._read(source)
         else:
             img = np.asarray(source, np.uint8)
@@ -237,6 +243,15 @@ class EnvLight:
         self.rgba = np.ascontiguousarray(img[::-1])           # bottom-up
         h, w = self.rgba.shape[:2]
         check(lib().tpt_env_create(_ptr(self.rgba), w, h, device, C.byref(self.handle)))
+
+    @staticmethod
+    def _native(path):
+        try:
+            with open(path, "rb") as f:
+                head = f.read(2)
+        except OSError as e:
+            raise RuntimeError(f"Failed to open file {path}") from e
+        return head in (b"\xff\xd8", b"P6")
 
     @staticmethod
     def _read(path):

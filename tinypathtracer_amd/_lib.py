@@ -79,6 +79,10 @@ SIGNATURES = [
     ("tpt_scene_destroy", None, [C.c_void_p]),
     ("tpt_env_create", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int, C.POINTER(C.c_void_p)]),
     ("tpt_env_destroy", None, [C.c_void_p]),
+    ("tpt_env_load", C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
+    ("tpt_image_load", C.c_int, [C.c_char_p, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_int32),
+                                 C.POINTER(C.c_int32)]),
+    ("tpt_image_free", None, [C.c_void_p]),
     ("tpt_render", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_void_p,
                              C.c_void_p, C.POINTER(Stats)]),
     ("tpt_render_frames", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(Camera), C.POINTER(Params), C.c_int32,

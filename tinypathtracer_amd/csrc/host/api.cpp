@@ -418,6 +418,41 @@ void tpt_env_destroy(tpt_env* env) {
     delete env;
 }
 
+tpt_status tpt_image_load(const char* path, uint8_t** rgba, int32_t* width, int32_t* height) {
+    if (!path || !rgba || !width || !height) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    *rgba = nullptr;
+    std::vector<uint8_t> px;
+    int w = 0, h = 0;
+    try {
+        tpt::load_image(path, px, w, h);
+    } catch (const tpt::io_error& e) {
+        return fail(TPT_ERR_IO, e.what());
+    } catch (const std::exception& e) {
+        return fail(TPT_ERR_PARSE, e.what());
+    }
+    uint8_t* buf = static_cast<uint8_t*>(std::malloc(px.size()));
+    if (!buf) return fail(TPT_ERR_OOM, "host allocation failed");
+    std::memcpy(buf, px.data(), px.size());
+    *rgba = buf;
+    *width = w;
+    *height = h;
+    return TPT_OK;
+}
+
+void tpt_image_free(uint8_t* rgba) { std::free(rgba); }
+
+tpt_status tpt_env_load(const char* path, int device, tpt_env** out) {
+    if (!path || !out) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    uint8_t* px = nullptr;
+    int32_t w = 0, h = 0;
+    const tpt_status st = tpt_image_load(path, &px, &w, &h);
+    if (st != TPT_OK) return st;
+    const tpt_status st2 = tpt_env_create(px, w, h, device, out);
+    tpt_image_free(px);
+    return st2;
+}
+
 static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, tpt::TraceArgs& a) {
     a.inner = s->inner.p;
     a.inner4 = s->inner4.p;

@@ -42,6 +42,10 @@ struct HostScene {
 
 void load_gltf(const std::string& path, HostScene& hs);
 
+// Env-map image (JPEG / binary PPM) decoded as FreeImage + Texture would hand it
+// to the GPU: RGBA8, row 0 = bottom, RGB order, alpha 255 (image.cpp).
+void load_image(const std::string& path, std::vector<uint8_t>& rgba, int& w, int& h);
+
 }  // namespace tpt
 
 struct tpt_gltf {

@@ -4,7 +4,7 @@
 // (8-bit, copyToFB's truncating tone map) and the radiance as PFM (fp32).
 //
 //   tpt_render scene.gltf [--width W] [--height H] [--spp N] [--depth D]
-//              [--seed S] [--env equirect.ppm|--sky] [--out prefix] [--device i]
+//              [--seed S] [--env equirect.jpg|.ppm|--sky] [--out prefix] [--device i]
 //              [--frames F [--progressive]]
 #include <cmath>
 #include <cstdio>
@@ -18,24 +18,6 @@
 #include "tpt.hpp"
 
 namespace {
-
-bool read_ppm(const std::string& path, std::vector<uint8_t>& rgba, int& w, int& h) {
-    std::ifstream f(path, std::ios::binary);
-    std::string magic;
-    int maxv = 0;
-    if (!(f >> magic >> w >> h >> maxv) || magic != "P6" || maxv != 255) return false;
-    f.get();
-    std::vector<uint8_t> rgb((size_t)w * h * 3);
-    if (!f.read((char*)rgb.data(), (std::streamsize)rgb.size())) return false;
-    rgba.resize((size_t)w * h * 4);
-    for (size_t i = 0; i < (size_t)w * h; ++i) {
-        rgba[4 * i] = rgb[3 * i];
-        rgba[4 * i + 1] = rgb[3 * i + 1];
-        rgba[4 * i + 2] = rgb[3 * i + 2];
-        rgba[4 * i + 3] = 255;
-    }
-    return true;
-}
 
 // Deterministic procedural sky (stand-in for the missing kloppenheim_07 env,
 // SURVEY 8(d) C3); same formula as tinypathtracer_amd.procedural_sky.
@@ -67,7 +49,7 @@ std::vector<uint8_t> procedural_sky(int w, int h) {
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: %s scene.gltf [--width W] [--height H] [--spp N] [--depth D] [--seed S] "
-                             "[--env file.ppm | --sky] [--out prefix] [--device i] [--frames F [--progressive]]\n", argv[0]);
+                             "[--env file.jpg|file.ppm | --sky] [--out prefix] [--device i] [--frames F [--progressive]]\n", argv[0]);
         return 2;
     }
     std::string scene_file = argv[1], env_file, out = "out";
@@ -97,10 +79,7 @@ int main(int argc, char** argv) {
     try {
         tpt::EnvLight env;
         if (!env_file.empty()) {
-            std::vector<uint8_t> rgba;
-            int ew = 0, eh = 0;
-            if (!read_ppm(env_file, rgba, ew, eh)) throw std::runtime_error("Failed to open file " + env_file);
-            env = tpt::EnvLight(rgba.data(), ew, eh, device);
+            env = tpt::EnvLight(env_file, device);   // JPEG / PPM, decoded natively (tpt_env_load)
         } else if (sky) {
             auto img = procedural_sky(2048, 1024);
             env = tpt::EnvLight(img.data(), 2048, 1024, device);
