@@ -2,7 +2,7 @@
 # Interleaved A/B: for each repetition and argument line, run libtpt.so and every
 # variant back to back (same box, same thermal state); prints one line per run.
 set -o pipefail
-libs="tinypathtracer_amd/libtpt.so $(ls tinypathtracer_amd/variants/*/libtpt.so 2>/dev/null)"
+libs=${LIBS:-"tinypathtracer_amd/libtpt.so $(ls tinypathtracer_amd/variants/*/libtpt.so 2>/dev/null)"}
 for rep in $(seq ${REPS:-2}); do
   while IFS= read -r line; do
     [ -z "$line" ] && continue
