@@ -93,6 +93,8 @@ SIGNATURES = [
     ("tpt_debug_rng_init", C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]),
     ("tpt_debug_trace_rays", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p]),
+    ("tpt_wide_tree_build", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                        C.POINTER(C.c_int32)]),
     ("tpt_gltf_load", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
     ("tpt_gltf_desc", C.c_int, [C.c_void_p, C.POINTER(SceneDesc), C.POINTER(Camera)]),
     ("tpt_gltf_missing_material", C.c_int, [C.c_void_p]),

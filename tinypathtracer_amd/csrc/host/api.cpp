@@ -166,6 +166,7 @@ struct tpt_scene {
     int32_t boxes_finite = 0;
     int32_t any_emitter = 1;                // some triangle's material has emissionFactor != 0
     int32_t n4 = 0;
+    int32_t wide_tree = 0;                  // 1: inner4 holds the SAH 4-wide tree (wide_bvh.cpp)
     uint32_t tree_depth = 0;
     // inputs
     DevBuf<uint32_t> indices;
@@ -373,9 +374,34 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     }
     // Stack capacity: the binary DFS that pushes one sibling per level holds at
     // most depth + 1 entries; the 4-wide ordered traversal pushes up to 3 per
-    // 4-wide node, one per two levels: 3 * ceil(depth / 2).
+    // 4-wide node: 3 * (4-wide levels) (the LBVH's even-depth view has
+    // ceil(depth / 2) of them).
     const uint32_t td = b.out_max_depth;
-    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, 3 * ((td + 1) / 2) + 1), 2);
+    uint32_t wide_levels = (td + 1) / 2;
+    s->wide_tree = 0;
+    const char* wt = std::getenv("TPT_WIDE_TREE");   // "lbvh": keep the even-depth view (A/B runs)
+    if (n > 1 && s->boxes_finite && !(wt && std::strcmp(wt, "lbvh") == 0)) {
+        // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
+        std::vector<float> lbox(6 * n);
+        std::vector<uint32_t> lemit(n);
+        HIP_OR_FAIL(hipMemcpyAsync(lbox.data(), s->node_box.p + 6 * (n - 1), 6 * n * sizeof(float),
+                                   hipMemcpyDeviceToHost, s->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(lemit.data(), s->emit.p + (n - 1), n * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   s->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+        std::vector<float> w4;
+        int levels = 0;
+        const int n4 = tpt::build_wide_sah((int)n, lbox.data(), lemit.data(), w4, &levels);
+        if (n4 > 0 && (size_t)n4 <= n - 1 && 3 * (uint32_t)levels + 1 <= 160) {
+            HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, w4.data(), w4.size() * sizeof(float), hipMemcpyHostToDevice,
+                                       s->stream));
+            HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+            s->n4 = n4;
+            wide_levels = (uint32_t)levels;
+            s->wide_tree = 1;
+        }
+    }
+    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, 3 * wide_levels + 1), 2);
     if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
     s->built = true;
     return TPT_OK;

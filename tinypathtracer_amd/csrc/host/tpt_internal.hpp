@@ -46,6 +46,10 @@ void load_gltf(const std::string& path, HostScene& hs);
 // to the GPU: RGBA8, row 0 = bottom, RGB order, alpha 255 (image.cpp).
 void load_image(const std::string& path, std::vector<uint8_t>& rgba, int& w, int& h);
 
+// SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp):
+// 32 floats per node in the inner4 layout; returns the node count.
+int build_wide_sah(int n, const float* leaf_box, const uint32_t* leaf_emit, std::vector<float>& out, int* levels);
+
 }  // namespace tpt
 
 struct tpt_gltf {

@@ -1,0 +1,332 @@
+// wide_bvh.cpp -- the 4-wide traversal tree of the ordered traversal, built on
+// the host with the surface-area heuristic over the LBVH's exact leaf boxes.
+//
+// Why a second tree is exact.  For a finite ray and finite boxes, the
+// reference (traverseBVH, path_tracer.cu:61-107) reaches a leaf iff the leaf's
+// own box passes rayHitBBox (geometry_queries.h:18-46): every ancestor box is
+// the exact min/max union of boxes that contain it and the slab arithmetic is
+// monotonic in the bounds, so an ancestor passes whenever the leaf does.  The
+// closest hit is then "least t > Delta, ties to the leaf met first", and the
+// right-first DFS meets leaves in decreasing sorted position.  None of this
+// depends on the tree's inner nodes: any hierarchy whose leaves carry the
+// reference's leaf boxes (bvh.cu:128-148, the LBVH build's node_box) and
+// positions finds the same hit under the kernel's ordered tie rule (equal t ->
+// larger position).  Its inner boxes only steer the walk and cull, so they may
+// be any supersets; here they are exact unions.
+//
+// The LBVH's Morton split ignores triangle sizes (large wall triangles straddle
+// many splits) and its even-depth 4-wide view leaves many nodes with 2-3
+// children.  This tree splits by binned SAH and collapses to 4 children per
+// node by opening the largest-area internal child first.
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace tpt {
+
+namespace {
+
+// cost of a triangle test relative to a 4-wide node visit (collapse DP)
+constexpr double kWideCTri = 0.5;
+
+struct Box {
+    float lo[3], hi[3];
+    void empty() {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = __builtin_inff();
+            hi[k] = -__builtin_inff();
+        }
+    }
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    double area() const {
+        const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+        if (!(dx >= 0.0) || !(dy >= 0.0) || !(dz >= 0.0)) return 0.0;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct BNode {          // binary SAH node
+    Box box;
+    int left = -1, right = -1;   // child BNode ids; a leaf has left = -1
+    int pos = -1;                // leaf: the LBVH sorted position of its triangle
+    uint32_t emit = 0;
+};
+
+struct Builder {
+    const float* lbox;    // 6 per position
+    std::vector<BNode> nodes;
+    std::vector<int> idx;
+    std::vector<float> cen;   // 3 per position
+
+    Box leaf_box(int p) const {
+        Box b;
+        for (int k = 0; k < 3; ++k) {
+            b.lo[k] = lbox[6 * p + k];
+            b.hi[k] = lbox[6 * p + 3 + k];
+        }
+        return b;
+    }
+
+    // Splits idx[b, e) in place; returns the split point (b < m < e).
+    int split(int b, int e) {
+        const int m = e - b;
+        Box cb;
+        cb.empty();
+        for (int i = b; i < e; ++i)
+            for (int k = 0; k < 3; ++k) {
+                cb.lo[k] = std::min(cb.lo[k], cen[3 * idx[i] + k]);
+                cb.hi[k] = std::max(cb.hi[k], cen[3 * idx[i] + k]);
+            }
+        double best = __builtin_inf();
+        int best_axis = -1, best_m = -1;
+        if (m <= 32) {
+            // exact sweep over sorted centroids on each axis
+            std::vector<int> tmp(idx.begin() + b, idx.begin() + e);
+            std::vector<double> right_area(m);
+            for (int axis = 0; axis < 3; ++axis) {
+                std::stable_sort(tmp.begin(), tmp.end(), [&](int x, int y) {
+                    return cen[3 * x + axis] < cen[3 * y + axis];
+                });
+                Box acc;
+                acc.empty();
+                for (int i = m - 1; i > 0; --i) {
+                    acc.grow(leaf_box(tmp[i]));
+                    right_area[i] = acc.area();
+                }
+                acc.empty();
+                for (int i = 1; i < m; ++i) {
+                    acc.grow(leaf_box(tmp[i - 1]));
+                    const double c = acc.area() * i + right_area[i] * (m - i);
+                    if (c < best) {
+                        best = c;
+                        best_axis = axis;
+                        best_m = i;
+                    }
+                }
+            }
+            std::stable_sort(idx.begin() + b, idx.begin() + e, [&](int x, int y) {
+                return cen[3 * x + best_axis] < cen[3 * y + best_axis];
+            });
+            return b + best_m;
+        }
+        constexpr int kBins = 32;
+        for (int axis = 0; axis < 3; ++axis) {
+            const float ext = cb.hi[axis] - cb.lo[axis];
+            if (!(ext > 0.0f)) continue;
+            Box bb[kBins];
+            int bn[kBins] = {};
+            for (auto& x : bb) x.empty();
+            const float sc = kBins / ext;
+            for (int i = b; i < e; ++i) {
+                int k = (int)((cen[3 * idx[i] + axis] - cb.lo[axis]) * sc);
+                k = std::min(std::max(k, 0), kBins - 1);
+                ++bn[k];
+                bb[k].grow(leaf_box(idx[i]));
+            }
+            double ra[kBins];
+            int rn[kBins];
+            Box acc;
+            acc.empty();
+            int cnt = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                acc.grow(bb[k]);
+                cnt += bn[k];
+                ra[k] = acc.area();
+                rn[k] = cnt;
+            }
+            acc.empty();
+            cnt = 0;
+            for (int k = 1; k < kBins; ++k) {
+                acc.grow(bb[k - 1]);
+                cnt += bn[k - 1];
+                if (cnt == 0 || rn[k] == 0) continue;
+                const double c = acc.area() * cnt + ra[k] * rn[k];
+                if (c < best) {
+                    best = c;
+                    best_axis = axis;
+                    best_m = k;
+                }
+            }
+        }
+        if (best_axis < 0) {   // all centroids coincide: halve by position
+            std::sort(idx.begin() + b, idx.begin() + e);
+            return b + m / 2;
+        }
+        const float sc = kBins / (cb.hi[best_axis] - cb.lo[best_axis]);
+        auto mid = std::stable_partition(idx.begin() + b, idx.begin() + e, [&](int p) {
+            int k = (int)((cen[3 * p + best_axis] - cb.lo[best_axis]) * sc);
+            k = std::min(std::max(k, 0), kBins - 1);
+            return k < best_m;
+        });
+        int s = (int)(mid - idx.begin());
+        if (s == b || s == e) s = b + m / 2;
+        return s;
+    }
+
+    int build(int b, int e, const uint32_t* emit) {
+        const int id = (int)nodes.size();
+        nodes.emplace_back();
+        if (e - b == 1) {
+            nodes[id].pos = idx[b];
+            nodes[id].box = leaf_box(idx[b]);
+            nodes[id].emit = emit[idx[b]] ? 1u : 0u;
+            return id;
+        }
+        const int s = split(b, e);
+        const int l = build(b, s, emit);
+        const int r = build(s, e, emit);
+        nodes[id].left = l;
+        nodes[id].right = r;
+        nodes[id].box = nodes[l].box;
+        nodes[id].box.grow(nodes[r].box);
+        nodes[id].emit = nodes[l].emit | nodes[r].emit;
+        return id;
+    }
+};
+
+}  // namespace
+
+// n leaves (n >= 2); leaf_box[6n] by LBVH sorted position (min.xyz, max.xyz);
+// leaf_emit[n].  Writes 32 floats per 4-wide node in the inner4 layout of
+// device_api.hpp (breadth-first, root 0; child links: a 4-wide id, or n-1 +
+// position for a leaf, with the emitter flag in bit 30; -1 none) and returns
+// the node count; *levels = the number of 4-wide levels.
+int build_wide_sah(int n, const float* leaf_box, const uint32_t* leaf_emit, std::vector<float>& out, int* levels) {
+    Builder B;
+    B.lbox = leaf_box;
+    B.idx.resize(n);
+    B.cen.resize(3 * (size_t)n);
+    for (int p = 0; p < n; ++p) {
+        B.idx[p] = p;
+        for (int k = 0; k < 3; ++k) B.cen[3 * p + k] = 0.5f * (leaf_box[6 * p + k] + leaf_box[6 * p + 3 + k]);
+    }
+    B.nodes.reserve(2 * (size_t)n);
+    const int root = B.build(0, n, leaf_emit);
+    const auto& N = B.nodes;
+
+    // Collapse to 4-wide nodes by dynamic programming over the binary tree
+    // (the SAH cost of Ylitie et al. 2017's wide-BVH collapse, 1 triangle per
+    // leaf): D[x][k] is the least cost of representing subtree x as a forest
+    // of at most k subtrees, where a leaf costs c_tri * area (its triangle test
+    // runs when its box passes) and a subtree kept whole costs c_node * area
+    // plus the best 4-way forest of its children.  Greedy opening of the
+    // largest child leaves the bottom levels with 2-leaf nodes; the DP pulls
+    // leaves up into their grandparents.
+    const double c_node = 1.0, c_tri = kWideCTri;
+    const size_t nb = N.size();
+    std::vector<std::array<double, 5>> D(nb);
+    std::vector<std::array<int8_t, 5>> pick(nb);   // k >= 2: left share of the split (0: keep whole)
+    for (size_t x = nb; x-- > 0;) {                  // children have larger ids (pre-order)
+        const BNode& c = N[x];
+        if (c.left < 0) {
+            for (int k = 1; k <= 4; ++k) D[x][k] = c_tri * c.box.area();
+            continue;
+        }
+        auto forest = [&](int k, int8_t& a_best) {
+            double best = __builtin_inf();
+            for (int a = 1; a < k; ++a) {
+                const double v = D[c.left][a] + D[c.right][k - a];
+                if (v < best) {
+                    best = v;
+                    a_best = (int8_t)a;
+                }
+            }
+            return best;
+        };
+        int8_t a4 = 1;
+        const double whole = c_node * c.box.area() + forest(4, a4);
+        pick[x][1] = a4;   // the split of a node kept whole (its own 4-wide node)
+        D[x][1] = whole;
+        for (int k = 2; k <= 4; ++k) {
+            int8_t a = 1;
+            const double f = forest(k, a);
+            if (f < whole) {
+                D[x][k] = f;
+                pick[x][k] = a;
+            } else {
+                D[x][k] = whole;
+                pick[x][k] = 0;
+            }
+        }
+    }
+    struct Wide {
+        int kids[4];
+        int nk;
+        int level;
+    };
+    std::vector<Wide> wide;
+    std::vector<int> wide_of(nb, -1);
+    std::vector<int> queue{root};   // breadth-first over binary nodes that become 4-wide nodes
+    std::vector<int> qlevel{0};
+    int maxlevel = 0;
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int b = queue[qi];
+        Wide w{};
+        w.nk = 0;
+        w.level = qlevel[qi];
+        // expand (x, k): x's children as a forest of at most k roots
+        struct Item {
+            int x, k;
+        };
+        Item st[8];
+        int sp = 0;
+        st[sp++] = {N[b].right, 4 - pick[b][1]};
+        st[sp++] = {N[b].left, pick[b][1]};
+        while (sp > 0) {
+            const Item it = st[--sp];
+            const BNode& c = N[it.x];
+            const int a = (c.left >= 0 && it.k >= 2) ? pick[it.x][it.k] : 0;
+            if (a == 0) {
+                w.kids[w.nk++] = it.x;
+            } else {
+                st[sp++] = {c.right, it.k - a};
+                st[sp++] = {c.left, a};
+            }
+        }
+        wide_of[b] = (int)wide.size();
+        wide.push_back(w);
+        maxlevel = std::max(maxlevel, w.level);
+        for (int k = 0; k < w.nk; ++k)
+            if (N[w.kids[k]].left >= 0) {
+                queue.push_back(w.kids[k]);
+                qlevel.push_back(w.level + 1);
+            }
+    }
+    out.assign(32 * wide.size(), 0.0f);
+    for (size_t i = 0; i < wide.size(); ++i) {
+        float* q = out.data() + 32 * i;
+        int32_t links[4] = {-1, -1, -1, -1};
+        for (int k = 0; k < wide[i].nk; ++k) {
+            const BNode& c = N[wide[i].kids[k]];
+            for (int j = 0; j < 3; ++j) {
+                q[6 * k + j] = c.box.lo[j];
+                q[6 * k + 3 + j] = c.box.hi[j];
+            }
+            const int32_t id = c.left >= 0 ? wide_of[wide[i].kids[k]] : (n - 1) + c.pos;
+            links[k] = id | (int32_t)(c.emit << 30);
+        }
+        std::memcpy(q + 24, links, sizeof links);
+    }
+    *levels = maxlevel + 1;
+    return (int)wide.size();
+}
+
+}  // namespace tpt
+
+extern "C" int32_t tpt_wide_tree_build(int32_t n, const float* leaf_box, const uint32_t* leaf_emit, float* nodes,
+                                       int32_t cap, int32_t* levels) {
+    if (n < 2 || !leaf_box || !leaf_emit || cap < 0) return -1;
+    std::vector<float> out;
+    int lv = 0;
+    const int n4 = tpt::build_wide_sah(n, leaf_box, leaf_emit, out, &lv);
+    if (levels) *levels = lv;
+    if (n4 <= cap && nodes) std::memcpy(nodes, out.data(), out.size() * sizeof(float));
+    return n4;
+}
