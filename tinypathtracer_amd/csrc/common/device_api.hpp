@@ -8,11 +8,14 @@
 //     the leaf at sorted position id-(F-1).  Bit 30 of every child link is
 //     set when that child's subtree holds an emissive triangle (inner and
 //     inner4); traversals mask it off.
-//   inner4[8*n4] float4  4-wide view for the ordered traversal: one node per
-//     even-depth internal node, numbered breadth-first (root 0), holding its up
-//     to 4 grandchildren (a leaf child stands for itself): child k box = floats
-//     6k..6k+5 of q0..q5 (min.xyz, max.xyz), q6 = child ids (-1: none; a 4-wide
-//     node id < F-1, or F-1 + leaf position).
+//   inner4[8*(F-1)] float4  4-wide nodes for the ordered traversal, numbered
+//     breadth-first: child k box = floats 6k..6k+5 of q0..q5 (min.xyz,
+//     max.xyz), q6 = child ids (-1: none; a 4-wide node id < F-1, or F-1 +
+//     leaf position).  Default (wide_bvh.cpp, host): an SAH tree over the
+//     LBVH's exact leaf boxes in [0, n4), then from emit_root a tree over the
+//     emissive triangles alone.  TPT_WIDE_TREE=lbvh: the LBVH's even-depth
+//     nodes, each holding its up to 4 grandchildren (a leaf child stands for
+//     itself).
 //   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
 //   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, 0), (n2.xyz, 0)
 //   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)
@@ -77,6 +80,7 @@ struct TraceArgs {
     int32_t refill;                      // leave the traversal loop below this many active lanes
     int32_t boxes_finite;                // all node boxes finite: min/max slab test is exact
     int32_t any_emitter;                 // some triangle emits (else a direct probe adds nothing)
+    int32_t emit_root;                   // inner4 id of the emissive-triangle tree (-1: none)
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
     int32_t stack_lds_slots;             // set by launch_trace: stack slots held in LDS (rest private)

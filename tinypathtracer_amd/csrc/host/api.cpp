@@ -167,6 +167,7 @@ struct tpt_scene {
     int32_t any_emitter = 1;                // some triangle's material has emissionFactor != 0
     int32_t n4 = 0;
     int32_t wide_tree = 0;                  // 1: inner4 holds the SAH 4-wide tree (wide_bvh.cpp)
+    int32_t emit_root = -1;                 // inner4 id of the emissive-triangle tree's root (-1: none)
     uint32_t tree_depth = 0;
     // inputs
     DevBuf<uint32_t> indices;
@@ -380,8 +381,8 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     uint32_t wide_levels = (td + 1) / 2;
     s->wide_tree = 0;
     const char* wt = std::getenv("TPT_WIDE_TREE");   // "lbvh": keep the even-depth view (A/B runs)
-    if (n > 1 && s->boxes_finite && !(wt && std::strcmp(wt, "lbvh") == 0)) {
-        // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
+    s->emit_root = -1;
+    if (n > 1 && s->boxes_finite) {
         std::vector<float> lbox(6 * n);
         std::vector<uint32_t> lemit(n);
         HIP_OR_FAIL(hipMemcpyAsync(lbox.data(), s->node_box.p + 6 * (n - 1), 6 * n * sizeof(float),
@@ -389,17 +390,43 @@ tpt_status tpt_scene_build(tpt_scene* s) {
         HIP_OR_FAIL(hipMemcpyAsync(lemit.data(), s->emit.p + (n - 1), n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    s->stream));
         HIP_OR_FAIL(hipStreamSynchronize(s->stream));
-        std::vector<float> w4;
-        int levels = 0;
-        const int n4 = tpt::build_wide_sah((int)n, lbox.data(), lemit.data(), w4, &levels);
-        if (n4 > 0 && (size_t)n4 <= n - 1 && 3 * (uint32_t)levels + 1 <= 160) {
-            HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, w4.data(), w4.size() * sizeof(float), hipMemcpyHostToDevice,
-                                       s->stream));
-            HIP_OR_FAIL(hipStreamSynchronize(s->stream));
-            s->n4 = n4;
-            wide_levels = (uint32_t)levels;
-            s->wide_tree = 1;
+        tpt::WideParams prm;   // tuning override for A/B runs
+        if (const char* v = std::getenv("TPT_WIDE_SWEEP")) prm.sweep_max = std::atoi(v);
+        const int leaf_base = (int)n - 1;
+        if (!(wt && std::strcmp(wt, "lbvh") == 0)) {
+            // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
+            std::vector<int> all(n);
+            for (size_t p = 0; p < n; ++p) all[p] = (int)p;
+            std::vector<float> w4;
+            int levels = 0;
+            const int n4 = tpt::build_wide_sah(all, lbox.data(), lemit.data(), leaf_base, 0, w4, &levels, prm);
+            if (n4 > 0 && (size_t)n4 <= n - 1 && 3 * (uint32_t)levels + 1 <= 160) {
+                HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, w4.data(), w4.size() * sizeof(float),
+                                           hipMemcpyHostToDevice, s->stream));
+                s->n4 = n4;
+                wide_levels = (uint32_t)levels;
+                s->wide_tree = 1;
+            }
         }
+        // The direct probe's first pass (closest emissive hit, trace.hip
+        // TM_EMIT) walks a tree over the emissive triangles alone, appended
+        // after the main tree's nodes: same exact leaf boxes and positions, so
+        // the same hit as the emitter-filtered walk of the whole tree.
+        std::vector<int> em;
+        for (size_t p = 0; p < n; ++p)
+            if (lemit[p]) em.push_back((int)p);
+        if (!em.empty()) {
+            std::vector<float> e4;
+            int elevels = 0;
+            const int ne4 = tpt::build_wide_sah(em, lbox.data(), lemit.data(), leaf_base, s->n4, e4, &elevels, prm);
+            if (ne4 > 0 && (size_t)(s->n4 + ne4) <= n - 1 && 3 * (uint32_t)elevels + 1 <= 160) {
+                HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p + 8 * (size_t)s->n4, e4.data(), e4.size() * sizeof(float),
+                                           hipMemcpyHostToDevice, s->stream));
+                s->emit_root = s->n4;
+                wide_levels = std::max(wide_levels, (uint32_t)elevels);
+            }
+        }
+        HIP_OR_FAIL(hipStreamSynchronize(s->stream));
     }
     s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, 3 * wide_levels + 1), 2);
     if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
@@ -493,6 +520,7 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.stack_depth = s->stack_depth;
     a.boxes_finite = s->boxes_finite;
     a.any_emitter = s->any_emitter;
+    a.emit_root = s->emit_root;
     a.env = env ? env->texels.p : nullptr;
     a.env_w = env ? env->w : 0;
     a.env_h = env ? env->h : 0;

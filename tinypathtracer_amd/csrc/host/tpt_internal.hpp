@@ -46,9 +46,13 @@ void load_gltf(const std::string& path, HostScene& hs);
 // to the GPU: RGBA8, row 0 = bottom, RGB order, alpha 255 (image.cpp).
 void load_image(const std::string& path, std::vector<uint8_t>& rgba, int& w, int& h);
 
-// SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp):
-// 32 floats per node in the inner4 layout; returns the node count.
-int build_wide_sah(int n, const float* leaf_box, const uint32_t* leaf_emit, std::vector<float>& out, int* levels);
+// SAH 4-wide traversal tree over (a subset of) the LBVH's exact leaf boxes
+// (wide_bvh.cpp): 32 floats per node in the inner4 layout; returns the node count.
+struct WideParams {
+    int sweep_max = 32;    // SAH ranges up to this size use an exact sweep, larger ones 32 bins
+};
+int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
+                   int id_base, std::vector<float>& out, int* levels, const WideParams& prm);
 
 }  // namespace tpt
 

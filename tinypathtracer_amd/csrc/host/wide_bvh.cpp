@@ -24,12 +24,11 @@
 #include <cstring>
 #include <vector>
 
+#include "tpt_internal.hpp"
+
 namespace tpt {
 
 namespace {
-
-// cost of a triangle test relative to a 4-wide node visit (collapse DP)
-constexpr double kWideCTri = 0.5;
 
 struct Box {
     float lo[3], hi[3];
@@ -61,6 +60,7 @@ struct BNode {          // binary SAH node
 
 struct Builder {
     const float* lbox;    // 6 per position
+    int sweep_max = 32;   // ranges up to this size split by an exact sweep, larger ones binned
     std::vector<BNode> nodes;
     std::vector<int> idx;
     std::vector<float> cen;   // 3 per position
@@ -86,7 +86,7 @@ struct Builder {
             }
         double best = __builtin_inf();
         int best_axis = -1, best_m = -1;
-        if (m <= 32) {
+        if (m <= sweep_max) {
             // exact sweep over sorted centroids on each axis
             std::vector<int> tmp(idx.begin() + b, idx.begin() + e);
             std::vector<double> right_area(m);
@@ -193,40 +193,58 @@ struct Builder {
 
 }  // namespace
 
-// n leaves (n >= 2); leaf_box[6n] by LBVH sorted position (min.xyz, max.xyz);
-// leaf_emit[n].  Writes 32 floats per 4-wide node in the inner4 layout of
-// device_api.hpp (breadth-first, root 0; child links: a 4-wide id, or n-1 +
-// position for a leaf, with the emitter flag in bit 30; -1 none) and returns
-// the node count; *levels = the number of 4-wide levels.
-int build_wide_sah(int n, const float* leaf_box, const uint32_t* leaf_emit, std::vector<float>& out, int* levels) {
+// Leaves: the LBVH sorted positions `pos` (all of them, or a subset such as the
+// emissive triangles); leaf_box[6 * p] / leaf_emit[p] by position p.  Writes 32
+// floats per 4-wide node in the inner4 layout of device_api.hpp (breadth-first,
+// root first; child links: id_base + a node's index, or leaf_base + position
+// for a leaf, with the emitter flag in bit 30; -1 none) and returns the node
+// count; *levels = the number of 4-wide levels.
+int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
+                   int id_base, std::vector<float>& out, int* levels, const WideParams& prm) {
+    const int n = (int)pos.size();
+    out.clear();
+    *levels = 0;
+    if (n == 0) return 0;
     Builder B;
     B.lbox = leaf_box;
-    B.idx.resize(n);
-    B.cen.resize(3 * (size_t)n);
-    for (int p = 0; p < n; ++p) {
-        B.idx[p] = p;
+    B.sweep_max = prm.sweep_max;
+    B.idx = pos;
+    int pmax = 0;
+    for (int p : pos) pmax = std::max(pmax, p);
+    B.cen.resize(3 * (size_t)(pmax + 1));
+    for (int p : pos)
         for (int k = 0; k < 3; ++k) B.cen[3 * p + k] = 0.5f * (leaf_box[6 * p + k] + leaf_box[6 * p + 3 + k]);
-    }
     B.nodes.reserve(2 * (size_t)n);
     const int root = B.build(0, n, leaf_emit);
     const auto& N = B.nodes;
+    if (N[root].left < 0) {   // a single leaf: one node holding it
+        out.assign(32, 0.0f);
+        for (int j = 0; j < 3; ++j) {
+            out[j] = N[root].box.lo[j];
+            out[3 + j] = N[root].box.hi[j];
+        }
+        const int32_t links[4] = {(leaf_base + N[root].pos) | (int32_t)(N[root].emit << 30), -1, -1, -1};
+        std::memcpy(out.data() + 24, links, sizeof links);
+        *levels = 1;
+        return 1;
+    }
 
     // Collapse to 4-wide nodes by dynamic programming over the binary tree
     // (the SAH cost of Ylitie et al. 2017's wide-BVH collapse, 1 triangle per
     // leaf): D[x][k] is the least cost of representing subtree x as a forest
-    // of at most k subtrees, where a leaf costs c_tri * area (its triangle test
-    // runs when its box passes) and a subtree kept whole costs c_node * area
-    // plus the best 4-way forest of its children.  Greedy opening of the
-    // largest child leaves the bottom levels with 2-leaf nodes; the DP pulls
-    // leaves up into their grandparents.
-    const double c_node = 1.0, c_tri = kWideCTri;
+    // of at most k subtrees.  Every leaf is some node's child exactly once, so
+    // its triangle-test cost (area-weighted) is the same in every collapse and
+    // drops out; a subtree kept whole costs its area (the probability that its
+    // 4-wide node is visited) plus the best 4-way forest of its children.
+    // Greedy opening of the largest child leaves the bottom levels with 2-leaf
+    // nodes; the DP pulls leaves up into their grandparents.
     const size_t nb = N.size();
     std::vector<std::array<double, 5>> D(nb);
     std::vector<std::array<int8_t, 5>> pick(nb);   // k >= 2: left share of the split (0: keep whole)
     for (size_t x = nb; x-- > 0;) {                  // children have larger ids (pre-order)
         const BNode& c = N[x];
         if (c.left < 0) {
-            for (int k = 1; k <= 4; ++k) D[x][k] = c_tri * c.box.area();
+            for (int k = 1; k <= 4; ++k) D[x][k] = 0.0;
             continue;
         }
         auto forest = [&](int k, int8_t& a_best) {
@@ -241,7 +259,7 @@ int build_wide_sah(int n, const float* leaf_box, const uint32_t* leaf_emit, std:
             return best;
         };
         int8_t a4 = 1;
-        const double whole = c_node * c.box.area() + forest(4, a4);
+        const double whole = c.box.area() + forest(4, a4);
         pick[x][1] = a4;   // the split of a node kept whole (its own 4-wide node)
         D[x][1] = whole;
         for (int k = 2; k <= 4; ++k) {
@@ -309,7 +327,7 @@ int build_wide_sah(int n, const float* leaf_box, const uint32_t* leaf_emit, std:
                 q[6 * k + j] = c.box.lo[j];
                 q[6 * k + 3 + j] = c.box.hi[j];
             }
-            const int32_t id = c.left >= 0 ? wide_of[wide[i].kids[k]] : (n - 1) + c.pos;
+            const int32_t id = c.left >= 0 ? id_base + wide_of[wide[i].kids[k]] : leaf_base + c.pos;
             links[k] = id | (int32_t)(c.emit << 30);
         }
         std::memcpy(q + 24, links, sizeof links);
@@ -325,7 +343,9 @@ extern "C" int32_t tpt_wide_tree_build(int32_t n, const float* leaf_box, const u
     if (n < 2 || !leaf_box || !leaf_emit || cap < 0) return -1;
     std::vector<float> out;
     int lv = 0;
-    const int n4 = tpt::build_wide_sah(n, leaf_box, leaf_emit, out, &lv);
+    std::vector<int> pos(n);
+    for (int p = 0; p < n; ++p) pos[p] = p;
+    const int n4 = tpt::build_wide_sah(pos, leaf_box, leaf_emit, n - 1, 0, out, &lv, tpt::WideParams{});
     if (levels) *levels = lv;
     if (n4 <= cap && nodes) std::memcpy(nodes, out.data(), out.size() * sizeof(float));
     return n4;

@@ -40,7 +40,7 @@
 #define TPT_PROBE_SHORTCUT 1   // no emissive triangle: resolve direct probes in the shading pass
 #endif
 #ifndef TPT_LEAF_KB
-#define TPT_LEAF_KB 8     // run the triangle branch once this many lanes are blocked ...
+#define TPT_LEAF_KB 4     // run the triangle branch once this many lanes are blocked ...
 #endif
 #ifndef TPT_LEAF_KP
 #define TPT_LEAF_KP 24    // ... or this many lanes hold a parked leaf
@@ -117,8 +117,9 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 //   TM_ANY      shadow rays stop at the first accepted triangle (only
 //               hitIdx == -1 matters, :279)
 //   TM_EMIT     direct probe, pass 1: the closest hit among emissive triangles
-//               only -- children whose subtree holds no emitter (bit 30 of the
-//               link) are not entered
+//               only -- the 4-wide path walks the tree over the emissive
+//               triangles alone (a.emit_root); the binary path does not enter
+//               children whose subtree holds no emitter (bit 30 of the link)
 //   TM_OCCL     direct probe, pass 2 (after an emitter hit): any triangle that
 //               beats that hit (t, then leaf position) ends the ray as
 //               TM_OCCLUDED.  The probe only reads the closest hit's emission
@@ -138,7 +139,8 @@ struct Trav {
     bool fin;   // origin and 1/dir finite: no slab product can be NaN
 };
 
-__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool boxes_finite = false) {
+__device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool boxes_finite = false,
+                                           int emit_root = -1) {
     r.o = o;
     r.d = d;
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
@@ -153,6 +155,13 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
     r.mode = mode;
     r.fin = boxes_finite & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
             __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
+    if (mode == TM_EMIT && r.fin) {
+        // probe pass 1 on the 4-wide path walks the emissive-triangle tree; without
+        // one it becomes a plain closest-hit probe (the reference's own probe,
+        // whose closest hit may then be a non-emitter adding +0)
+        if (emit_root >= 0) r.node = emit_root;
+        else r.mode = TM_CLOSEST;
+    }
 }
 
 // Visit of inner node r.node: the child to descend into (-1: none) and, when
@@ -283,11 +292,10 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
     int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z), i3 = __float_as_int(q6.w);
     const float hd = 0.5f * kDelta;
     // a link is -1 (no child) or an id with the emitter flag in bit 30
-    const int need = r.mode == TM_EMIT ? (1 << 30) : 0;   // probe pass 1: emitter subtrees only
-    const bool h0 = (i0 >= 0) & ((i0 & need) == need) & (fmaxf(k0, hd) <= fminf(e0, hi));
-    const bool h1 = (i1 >= 0) & ((i1 & need) == need) & (fmaxf(k1, hd) <= fminf(e1, hi));
-    const bool h2 = (i2 >= 0) & ((i2 & need) == need) & (fmaxf(k2, hd) <= fminf(e2, hi));
-    const bool h3 = (i3 >= 0) & ((i3 & need) == need) & (fmaxf(k3, hd) <= fminf(e3, hi));
+    const bool h0 = (i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi));
+    const bool h1 = (i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi));
+    const bool h2 = (i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi));
+    const bool h3 = (i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi));
     i0 &= kLinkMask;
     i1 &= kLinkMask;
     i2 &= kLinkMask;
@@ -887,7 +895,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             if (ts != TS_DEAD) {
                 ++c_trav;
                 trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
-                           a.boxes_finite != 0);
+                           a.boxes_finite != 0, a.emit_root);
                 ts = TS_TRAV;
             }
             TPT_SEC(6)
