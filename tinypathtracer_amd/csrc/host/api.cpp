@@ -168,6 +168,7 @@ struct tpt_scene {
     int32_t n4 = 0;
     int32_t wide_tree = 0;                  // 1: inner4 holds the SAH 4-wide tree (wide_bvh.cpp)
     int32_t emit_root = -1;                 // inner4 id of the emissive-triangle tree's root (-1: none)
+    int32_t emit_inline = 0;                // that tree is one node of leaves (<= 4 emitters)
     uint32_t tree_depth = 0;
     // inputs
     DevBuf<uint32_t> indices;
@@ -382,6 +383,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     s->wide_tree = 0;
     const char* wt = std::getenv("TPT_WIDE_TREE");   // "lbvh": keep the even-depth view (A/B runs)
     s->emit_root = -1;
+    s->emit_inline = 0;
     if (n > 1 && s->boxes_finite) {
         std::vector<float> lbox(6 * n);
         std::vector<uint32_t> lemit(n);
@@ -423,6 +425,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
                 HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p + 8 * (size_t)s->n4, e4.data(), e4.size() * sizeof(float),
                                            hipMemcpyHostToDevice, s->stream));
                 s->emit_root = s->n4;
+                s->emit_inline = ne4 == 1 ? 1 : 0;
                 wide_levels = std::max(wide_levels, (uint32_t)elevels);
             }
         }
@@ -521,6 +524,7 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.boxes_finite = s->boxes_finite;
     a.any_emitter = s->any_emitter;
     a.emit_root = s->emit_root;
+    a.emit_inline = std::getenv("TPT_NO_EMIT_INLINE") ? 0 : s->emit_inline;   // env: A/B runs
     a.env = env ? env->texels.p : nullptr;
     a.env_w = env ? env->w : 0;
     a.env_h = env ? env->h : 0;

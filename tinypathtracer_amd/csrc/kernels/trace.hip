@@ -370,6 +370,29 @@ __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tr
     return take & ((r.mode == TM_ANY) | occl);
 }
 
+// Probe pass 1 over an emissive-triangle tree that is a single 4-wide node of
+// leaves (<= 4 emitters), run inside the shading pass instead of a traversal:
+// the node's leaf boxes by the same min/max slab test, then the triangle test
+// of every passing leaf.  The closest hit under the ordered tie rule does not
+// depend on the order the leaves are tested in, so r ends as the traversal
+// would leave it.
+__device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restrict__ nd,
+                                                  const float4* __restrict__ tri, int nint, uint32_t& c_leaf) {
+    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
+    float k0, k1, k2, k3, e0, e1, e2, e3;
+    slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
+    slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
+    slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
+    slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
+    const float hd = 0.5f * kDelta, hi = kRealMax;   // nothing hit yet: r.t = FLT_MAX
+    const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
+              i3 = __float_as_int(q6.w);
+    if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint); }
+    if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint); }
+    if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint); }
+    if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint); }
+}
+
 // Returns false once the traversal has finished (or overflowed its stack).
 // The stack region holds stack_depth + 1 slots so the push below may write
 // unconditionally (a write at sp == stack_depth lands in the spare slot).
@@ -737,6 +760,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             TPT_SEC_BEGIN()
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
+            bool begun = false;   // the next ray is already set up (inline probe pass 1)
             V3 L = v3(0.0f, 0.0f, 0.0f);
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
             if (phase == PH_EXT) {
@@ -817,6 +841,25 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             ++c_trav;
                             rec.put_dst(depth, mk, kNoProbe, direct);
                             after = true;
+                        } else if (ORDERED && a.emit_inline) {
+                            // <= 4 emitters: pass 1 here; a miss resolves the probe in
+                            // this pass, an emitter hit goes on to pass 2 (occlusion)
+                            ++c_trav;
+                            trav_begin(r, r.o, td, TM_EMIT, a.boxes_finite != 0, a.emit_root);
+                            begun = true;
+                            phase = PH_PROBE;
+                            if (r.mode == TM_EMIT && r.fin) {
+                                ++c_wide;
+                                emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf);
+                                if (r.fid < 0) {
+                                    rec.put_dst(depth, mk, kNoProbe, direct);
+                                    after = true;
+                                    begun = false;
+                                } else {
+                                    r.mode = TM_OCCL;
+                                    r.node = 0;
+                                }
+                            }
                         } else {
                             phase = PH_PROBE;
                         }
@@ -893,9 +936,11 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             }
             TPT_SEC(5)
             if (ts != TS_DEAD) {
-                ++c_trav;
-                trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
-                           a.boxes_finite != 0, a.emit_root);
+                if (!begun) {
+                    ++c_trav;
+                    trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
+                               a.boxes_finite != 0, a.emit_root);
+                }
                 ts = TS_TRAV;
             }
             TPT_SEC(6)
