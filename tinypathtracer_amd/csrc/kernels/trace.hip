@@ -632,7 +632,7 @@ struct PathRecords {
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
 // state (direct term, normal, light index, incoming direction -- r.d during an
 // extension ray) is dead across traversals and drops out of the registers.
-template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false>
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false>
 __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             ++c_trav;
                             rec.put_dst(depth, mk, kNoProbe, direct);
                             after = true;
-                        } else if (ORDERED && a.emit_inline) {
+                        } else if (INL) {
                             // <= 4 emitters: pass 1 here; a miss resolves the probe in
                             // this pass, an emitter hit goes on to pass 2 (occlusion)
                             ++c_trav;
@@ -1121,15 +1121,22 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
     }
 }
 
-template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false>
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false>
 static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL>), grid, dim3(256), lds, s, a);
 }
 
+// INL: probe pass 1 in the shading pass (an emissive tree of one node); its own
+// variant, so scenes with larger emitter sets keep the leaner kernel
 template <bool LIGHTS, bool MTL_LDS, typename StackT>
 static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
-    else launch_one<64, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
+    if (a.emit_inline) {
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, false, true>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, false, true>(a, grid, lds, s);
+    } else {
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
+    }
 }
 
 // LDS per 256-lane workgroup: [material table][traversal stack][path records],
