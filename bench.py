@@ -315,6 +315,8 @@ def main():
             "config": config,
             "msamples_per_s": round(tot["samples"] / elapsed / 1e6, 2),
             "rays_per_sample": round(rays / max(tot["samples"], 1), 4),
+            "visits_per_ray": {k: round(l_tot[k] / max(l_tot["traversals"], 1), 3)
+                               for k in ("wide_visits", "internal_visits", "leaf_tests")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
