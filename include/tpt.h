@@ -189,9 +189,10 @@ tpt_status tpt_debug_trace_rays(tpt_scene* scene, uint32_t n, const float* origi
 /* Host-only: the SAH 4-wide traversal tree tpt_scene_build uploads, over n >= 2
  * leaf boxes (6 floats each, by LBVH sorted position) and emitter flags.  Writes
  * at most `cap` nodes of 32 floats (inner4 layout, device_api.hpp) and the
- * number of 4-wide levels; returns the node count (> cap: not written), or -1. */
+ * most stack entries its ordered walk can hold; returns the node count (> cap:
+ * not written), or -1. */
 int32_t tpt_wide_tree_build(int32_t n, const float* leaf_box, const uint32_t* leaf_emit, float* nodes,
-                            int32_t cap, int32_t* levels);
+                            int32_t cap, int32_t* stack_need);
 
 /* ---- host-side glTF loader (mesh.cu:80-397 semantics) -------------------- */
 typedef struct tpt_gltf tpt_gltf;

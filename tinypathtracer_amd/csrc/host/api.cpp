@@ -375,11 +375,10 @@ tpt_status tpt_scene_build(tpt_scene* s) {
         s->any_emitter = root_emit != 0 ? 1 : 0;
     }
     // Stack capacity: the binary DFS that pushes one sibling per level holds at
-    // most depth + 1 entries; the 4-wide ordered traversal pushes up to 3 per
-    // 4-wide node: 3 * (4-wide levels) (the LBVH's even-depth view has
-    // ceil(depth / 2) of them).
+    // most depth + 1 entries; the 4-wide ordered walk holds at most the tree's
+    // stack need (wide_bvh.cpp), 3 * ceil(depth / 2) for the LBVH's even-depth view.
     const uint32_t td = b.out_max_depth;
-    uint32_t wide_levels = (td + 1) / 2;
+    uint32_t wide_need = 3 * ((td + 1) / 2) + 1;
     s->wide_tree = 0;
     const char* wt = std::getenv("TPT_WIDE_TREE");   // "lbvh": keep the even-depth view (A/B runs)
     s->emit_root = -1;
@@ -400,13 +399,13 @@ tpt_status tpt_scene_build(tpt_scene* s) {
             std::vector<int> all(n);
             for (size_t p = 0; p < n; ++p) all[p] = (int)p;
             std::vector<float> w4;
-            int levels = 0;
-            const int n4 = tpt::build_wide_sah(all, lbox.data(), lemit.data(), leaf_base, 0, w4, &levels, prm);
-            if (n4 > 0 && (size_t)n4 <= n - 1 && 3 * (uint32_t)levels + 1 <= 160) {
+            int need = 0;
+            const int n4 = tpt::build_wide_sah(all, lbox.data(), lemit.data(), leaf_base, 0, w4, &need, prm);
+            if (n4 > 0 && (size_t)n4 <= n - 1 && need <= 150) {
                 HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, w4.data(), w4.size() * sizeof(float),
                                            hipMemcpyHostToDevice, s->stream));
                 s->n4 = n4;
-                wide_levels = (uint32_t)levels;
+                wide_need = (uint32_t)need;
                 s->wide_tree = 1;
             }
         }
@@ -419,19 +418,19 @@ tpt_status tpt_scene_build(tpt_scene* s) {
             if (lemit[p]) em.push_back((int)p);
         if (!em.empty()) {
             std::vector<float> e4;
-            int elevels = 0;
-            const int ne4 = tpt::build_wide_sah(em, lbox.data(), lemit.data(), leaf_base, s->n4, e4, &elevels, prm);
-            if (ne4 > 0 && (size_t)(s->n4 + ne4) <= n - 1 && 3 * (uint32_t)elevels + 1 <= 160) {
+            int eneed = 0;
+            const int ne4 = tpt::build_wide_sah(em, lbox.data(), lemit.data(), leaf_base, s->n4, e4, &eneed, prm);
+            if (ne4 > 0 && (size_t)(s->n4 + ne4) <= n - 1 && eneed <= 150) {
                 HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p + 8 * (size_t)s->n4, e4.data(), e4.size() * sizeof(float),
                                            hipMemcpyHostToDevice, s->stream));
                 s->emit_root = s->n4;
                 s->emit_inline = ne4 == 1 ? 1 : 0;
-                wide_levels = std::max(wide_levels, (uint32_t)elevels);
+                wide_need = std::max(wide_need, (uint32_t)eneed);
             }
         }
         HIP_OR_FAIL(hipStreamSynchronize(s->stream));
     }
-    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, 3 * wide_levels + 1), 2);
+    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, wide_need), 2);
     if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
     s->built = true;
     return TPT_OK;

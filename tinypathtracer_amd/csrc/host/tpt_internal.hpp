@@ -52,7 +52,7 @@ struct WideParams {
     int sweep_max = 32;    // SAH ranges up to this size use an exact sweep, larger ones 32 bins
 };
 int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
-                   int id_base, std::vector<float>& out, int* levels, const WideParams& prm);
+                   int id_base, std::vector<float>& out, int* stack_need, const WideParams& prm);
 
 }  // namespace tpt
 

@@ -198,12 +198,13 @@ struct Builder {
 // floats per 4-wide node in the inner4 layout of device_api.hpp (breadth-first,
 // root first; child links: id_base + a node's index, or leaf_base + position
 // for a leaf, with the emitter flag in bit 30; -1 none) and returns the node
-// count; *levels = the number of 4-wide levels.
+// count; *stack_need = the most stack entries the ordered 4-wide walk can hold
+// right after a visit (trace.hip inner_visit4; see below).
 int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
-                   int id_base, std::vector<float>& out, int* levels, const WideParams& prm) {
+                   int id_base, std::vector<float>& out, int* stack_need, const WideParams& prm) {
     const int n = (int)pos.size();
     out.clear();
-    *levels = 0;
+    *stack_need = 0;
     if (n == 0) return 0;
     Builder B;
     B.lbox = leaf_box;
@@ -225,7 +226,7 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
         }
         const int32_t links[4] = {(leaf_base + N[root].pos) | (int32_t)(N[root].emit << 30), -1, -1, -1};
         std::memcpy(out.data() + 24, links, sizeof links);
-        *levels = 1;
+        *stack_need = 0;
         return 1;
     }
 
@@ -274,21 +275,25 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
             }
         }
     }
+    // Stack bound: a visit of node X finds at most A(X) entries on the stack --
+    // the deferred siblings of X and of its ancestors, A(X) = sum over the
+    // proper ancestors a of (children(a) - 1) -- and leaves at most A(X) +
+    // children(X) - 1.
     struct Wide {
         int kids[4];
         int nk;
-        int level;
+        int above;   // A(X)
     };
     std::vector<Wide> wide;
     std::vector<int> wide_of(nb, -1);
     std::vector<int> queue{root};   // breadth-first over binary nodes that become 4-wide nodes
-    std::vector<int> qlevel{0};
-    int maxlevel = 0;
+    std::vector<int> qabove{0};
+    int need = 0;
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const int b = queue[qi];
         Wide w{};
         w.nk = 0;
-        w.level = qlevel[qi];
+        w.above = qabove[qi];
         // expand (x, k): x's children as a forest of at most k roots
         struct Item {
             int x, k;
@@ -310,11 +315,11 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
         }
         wide_of[b] = (int)wide.size();
         wide.push_back(w);
-        maxlevel = std::max(maxlevel, w.level);
+        need = std::max(need, w.above + w.nk - 1);
         for (int k = 0; k < w.nk; ++k)
             if (N[w.kids[k]].left >= 0) {
                 queue.push_back(w.kids[k]);
-                qlevel.push_back(w.level + 1);
+                qabove.push_back(w.above + w.nk - 1);
             }
     }
     out.assign(32 * wide.size(), 0.0f);
@@ -332,21 +337,21 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
         }
         std::memcpy(q + 24, links, sizeof links);
     }
-    *levels = maxlevel + 1;
+    *stack_need = need;
     return (int)wide.size();
 }
 
 }  // namespace tpt
 
 extern "C" int32_t tpt_wide_tree_build(int32_t n, const float* leaf_box, const uint32_t* leaf_emit, float* nodes,
-                                       int32_t cap, int32_t* levels) {
+                                       int32_t cap, int32_t* stack_need) {
     if (n < 2 || !leaf_box || !leaf_emit || cap < 0) return -1;
     std::vector<float> out;
     int lv = 0;
     std::vector<int> pos(n);
     for (int p = 0; p < n; ++p) pos[p] = p;
     const int n4 = tpt::build_wide_sah(pos, leaf_box, leaf_emit, n - 1, 0, out, &lv, tpt::WideParams{});
-    if (levels) *levels = lv;
+    if (stack_need) *stack_need = lv;
     if (n4 <= cap && nodes) std::memcpy(nodes, out.data(), out.size() * sizeof(float));
     return n4;
 }
