@@ -231,7 +231,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     keys = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
-            "rng_init_ms", "resolve_ms", "trace_launches"]
+            "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms"]
     local_tot = {k: float(sum(s[k] for s in stats)) for k in keys}
     vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64,
                        device=f"cuda:{dev}" if args.dist_backend == "nccl" else "cpu")
@@ -275,7 +275,10 @@ def main():
         bytes_total = (B_INNER * l_tot["internal_visits"] + B_WIDE * l_tot["wide_visits"] + B_LEAF * l_tot["leaf_tests"] +
                        B_HIT * l_tot["shade_hits"] + B_PIX * l_tot["pixels"])
         bytes_per_launch = bytes_total / nl
-        avg_launch_s = (l_tot["trace_ms"] / nl) / 1e3
+        # each launch's own duration (HIP events on its stream; what rocprofv3
+        # reports per kernel): the launch pipeline overlaps launches, so their
+        # sum exceeds the trace phase's wall time and this rate is conservative
+        avg_launch_s = (l_tot["trace_kernel_ms"] / nl) / 1e3
         achieved = bytes_per_launch / avg_launch_s / 1e9
         traffic = None
         batch = (f" x {n_frames} frames (seeds {seeds[0]}..{seeds[-1]}), each banded across {ranks} ranks"

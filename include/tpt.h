@@ -112,13 +112,15 @@ typedef struct {
     uint64_t pixels;              /* pixels rendered by this call */
     uint64_t samples;             /* pixels * spp */
     double rng_init_ms;           /* setupRandSeed equivalent */
-    double trace_ms;              /* sum over trace launches (HIP events) */
+    double trace_ms;              /* trace phase, first launch start to last launch end (HIP events) */
     double resolve_ms;            /* copyToFB equivalent */
     double total_ms;              /* whole tpt_render, host wall */
     int32_t trace_launches;
     int32_t pad;
     uint64_t wide_visits;         /* 4-wide internal nodes popped (ordered traversal) */
     uint64_t accumulated_spp;     /* samples per pixel in the output (> spp with TPT_FLAG_ACCUMULATE) */
+    double trace_kernel_ms;       /* sum of the trace launches' own durations (HIP events per launch);
+                                     > trace_ms when the launch pipeline overlaps them */
 } tpt_stats;
 
 typedef struct tpt_scene tpt_scene;

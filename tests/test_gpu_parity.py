@@ -269,6 +269,44 @@ def test_spp_chunking_bit_identical(built):
     assert np.array_equal(_bits(a), _bits(b))
 
 
+def test_launch_pipeline_bit_identical(built, monkeypatch):
+    """The launch pipeline (row band sets on their own streams, spp in offset
+    chunks, host/api.cpp; the default from 1024 spp on, TPT_PIPE forces it from
+    256) equals one launch bit for bit: 2, 3 and 4 sets, banded across ranks,
+    and a frame batch."""
+    s, d, _ = built["box"]
+    W, H, spp = 96, 80, 256
+    pt = T.PathTracer("", W, H, 0)
+    monkeypatch.setenv("TPT_PIPE", "1")
+    one = np.zeros((H, W, 3), np.float32)
+    fb1 = np.zeros((H, W, 4), np.uint8)
+    st1 = pt.doTrace(d, s.m_camera, fb1, spp, seed=11, radiance=one)
+    assert st1["trace_launches"] == 1
+    seeds = [11, 12]
+    batch1 = [np.zeros((H, W, 3), np.float32) for _ in seeds]
+    pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch1)
+    for sets, launches in ((2, 5), (3, 8), (4, 11)):   # chunks of 128 spp, set k k/sets of a chunk ahead
+        monkeypatch.setenv("TPT_PIPE", str(sets))
+        got = np.zeros((H, W, 3), np.float32)
+        fb = np.zeros((H, W, 4), np.uint8)
+        st = pt.doTrace(d, s.m_camera, fb, spp, seed=11, radiance=got)
+        assert st["trace_launches"] == launches, sets
+        assert st["traversals"] == st1["traversals"]
+        assert st["trace_kernel_ms"] > 0.0
+        assert np.array_equal(_bits(got), _bits(one)), sets
+        assert np.array_equal(fb, fb1), sets
+    monkeypatch.setenv("TPT_PIPE", "2")
+    banded = np.zeros((H, W, 3), np.float32)
+    for idx in range(2):
+        pt.doTrace(d, s.m_camera, None, spp, seed=11, radiance=banded, band=(16, 2, idx))
+    assert np.array_equal(_bits(banded), _bits(one))
+    batch = [np.zeros((H, W, 3), np.float32) for _ in seeds]
+    st = pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch)
+    assert st["trace_launches"] > 1
+    for f in range(len(seeds)):
+        assert np.array_equal(_bits(batch[f]), _bits(batch1[f])), f
+
+
 def test_progressive_accumulation_bit_identical(built):
     """TPT_FLAG_ACCUMULATE: 4 calls of 4 spp continue the same per-pixel streams
     and sums, so the frame equals one 16-spp call bit for bit; a changed frame

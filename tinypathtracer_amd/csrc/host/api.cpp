@@ -100,6 +100,9 @@ std::vector<uint32_t>& host_jumps() {
     return j;
 }
 
+constexpr int kMaxPipe = 4;         // overlapped launch sets per frame (GPU_MAX_HW_QUEUES is 4)
+constexpr int kPipeMinChunk = 128;  // spp per pipelined launch, at least
+
 int band_height_of(int height, int band_rows, int band_count, int band_index) {
     int n = 0;
     for (int y = 0; y < height; ++y)
@@ -195,12 +198,45 @@ struct tpt_scene {
     int acc_w = 0, acc_h = 0, acc_rows = 0, acc_count = 0, acc_index = 0;
     uint64_t acc_spp = 0;
     std::vector<uint64_t> acc_seeds;        // one per frame of the batch
+    // overlapped launch pipeline: extra streams (set k >= 1 of a frame's rows)
+    // and a pool of per-launch timing events
+    std::vector<hipStream_t> pipe;
+    std::vector<hipEvent_t> lev;
+    hipEvent_t pipe_ev[2 * kMaxPipe] = {};
 
     ~tpt_scene() {
         DeviceGuard g(device);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& e : lev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : pipe_ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& q : pipe)
+            if (q) (void)hipStreamDestroy(q);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    // streams for sets 1..n-1 and the fork/join events
+    hipError_t ensure_pipe(int n) {
+        hipError_t e = hipSuccess;
+        while (e == hipSuccess && (int)pipe.size() < n - 1) {
+            hipStream_t q = nullptr;
+            e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+            if (e == hipSuccess) pipe.push_back(q);
+        }
+        for (int i = 0; e == hipSuccess && i < 2 * kMaxPipe; ++i)
+            if (!pipe_ev[i]) e = hipEventCreateWithFlags(&pipe_ev[i], hipEventDisableTiming);
+        return e;
+    }
+    hipError_t ensure_launch_events(size_t n) {
+        hipError_t e = hipSuccess;
+        while (e == hipSuccess && lev.size() < n) {
+            hipEvent_t x = nullptr;
+            e = hipEventCreate(&x);
+            if (e == hipSuccess) lev.push_back(x);
+        }
+        return e;
     }
 };
 
@@ -619,37 +655,122 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;
+    // Launch schedule.  A launch ends in a tail where CUs drain: a wave's life
+    // is its heaviest pixel's serial chain (samples run in order on one lane),
+    // and the waves dispatched last (the top rows of the box) live ~40x longer
+    // than the miss tiles -- measured on box at 256 spp, 25 % of the launch's
+    // wave slots idle.  Default (spp >= 1024): the rows split into P = 3 interleaved band sets,
+    // each on its own stream, and the spp into chunks, set k's chunk boundaries
+    // offset by k/P of a chunk: while one set's launch drains, another set's
+    // launch is mid-flight and takes the freed slots.  A pixel's samples still
+    // run in order (its set's launches are stream-ordered, RNG and sums persist
+    // between chunks), so the result is bit-identical to one launch.
+    // TPT_PIPE=<P> (1: one stream), TPT_PIPE_CHUNKS=<chunks per set> override;
+    // an explicit spp_per_launch keeps the single-stream chunked loop.
+    int chunk = p->spp_per_launch;
+    int nset = 1;
+    if (chunk <= 0) {
+        // one stream: chunk only past ~4096 spp of 1080p pixels so one launch stays below ~5 s
+        const double band_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
+        chunk = (int)std::max(1.0, std::floor(4096.0 * 2073600.0 / band_pix));
+        const char* pe = std::getenv("TPT_PIPE");
+        const char* pc = std::getenv("TPT_PIPE_CHUNKS");
+        nset = pe ? std::atoi(pe) : 3;
+        const int per_set = std::max(pc ? std::atoi(pc) : 8, 1);
+        nset = std::max(1, std::min(nset, kMaxPipe));
+        // worth it only with several chunks of real work and rows for every set
+        if (bh < nset * band_rows) nset = 1;
+        // chunks of at least 128 spp, and by default only from 1024 spp on
+        // (measured on box 1080p, 3 sets: 1024 spp +6.7 %; 256 spp -2 %, 32-spp
+        // chunks -4 %: concurrently running launches at different rows cost
+        // locality, and every launch its prologue)
+        if (nset > 1) chunk = std::min(chunk, std::max(kPipeMinChunk, (p->spp + per_set - 1) / per_set));
+        if (p->spp < (pe ? 2 : 8) * kPipeMinChunk) nset = 1;
+    }
+    chunk = std::min(chunk, p->spp);
+    struct Launch {
+        int set, samples;
+    };
+    std::vector<Launch> plan;
+    for (int k = 0; k < nset; ++k) {
+        int done = 0;
+        const int first = chunk - (k * chunk) / nset;   // set k starts k/nset of a chunk early
+        for (int c = first; done < p->spp && bh > 0; c = chunk) {
+            const int n = std::min(c, p->spp - done);
+            plan.push_back({k, n});
+            done += n;
+        }
+    }
     a.debug_waves = nullptr;
     const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");   // phase-profiling builds only
-    const size_t dbg_words =
+    const size_t dbg_launch =
         8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 15) / 16) * nf;
+    const size_t dbg_words = dbg_launch * std::max<size_t>(plan.size(), 1);   // one region per launch
     if (dbg_path) {
         HIP_OR_FAIL(s->debug.alloc(dbg_words));
         HIP_OR_FAIL(hipMemsetAsync(s->debug.p, 0, dbg_words * sizeof(unsigned long long), st));
-        a.debug_waves = s->debug.p;
     }
-
-    int chunk = p->spp_per_launch;
-    if (chunk <= 0) {
-        // One launch per frame batch: every launch ends in a tail where CUs
-        // drain (measured ~7 ms per launch on box 1080p, 9% at 64-spp chunks).
-        // Chunk only past ~4096 spp of 1080p pixels so one launch stays below ~5 s.
-        const double band_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
-        chunk = (int)std::max(1.0, std::floor(4096.0 * 2073600.0 / band_pix));
+    HIP_OR_FAIL(s->ensure_launch_events(2 * plan.size()));
+    hipStream_t qs[kMaxPipe] = {st};
+    if (nset > 1) {
+        HIP_OR_FAIL(s->ensure_pipe(nset));
+        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[0], st));   // fork: RNG init and the sums' reset are done
+        for (int k = 1; k < nset; ++k) {
+            qs[k] = s->pipe[k - 1];
+            HIP_OR_FAIL(hipStreamWaitEvent(qs[k], s->pipe_ev[0], 0));
+        }
     }
-    chunk = std::min(chunk, p->spp);
-    double trace_ms = 0.0;
+    // set k renders bands band_index + k * band_count of the band_count * nset interleave
+    int set_bh[kMaxPipe] = {bh};
+    for (int k = 0; k < nset; ++k)
+        set_bh[k] = nset == 1 ? bh : band_height_of(H, band_rows, band_count * nset, p->band_index + k * band_count);
+    // issue the sets' launches interleaved in time order (chunk starts), so no
+    // stream's queue runs ahead of the others on the host side
+    std::vector<size_t> order(plan.size());
+    {
+        std::vector<double> t0(plan.size());
+        double at[kMaxPipe] = {};
+        for (size_t j = 0; j < plan.size(); ++j) {
+            t0[j] = at[plan[j].set];
+            at[plan[j].set] += plan[j].samples;
+        }
+        for (size_t j = 0; j < order.size(); ++j) order[j] = j;
+        std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return t0[x] < t0[y]; });
+    }
+    for (size_t oi = 0; oi < order.size(); ++oi) {
+        const size_t j = order[oi];
+        const int k = plan[j].set;
+        if (set_bh[k] <= 0) continue;
+        tpt::TraceArgs ak = a;
+        ak.samples = plan[j].samples;
+        if (nset > 1) {
+            ak.band_count = band_count * nset;
+            ak.band_index = p->band_index + k * band_count;
+            ak.band_height = set_bh[k];
+        }
+        if (dbg_path) ak.debug_waves = s->debug.p + oi * dbg_launch;
+        HIP_OR_FAIL(hipEventRecord(s->lev[2 * j], qs[k]));
+        HIP_OR_FAIL(tpt::launch_trace(ak, qs[k]));
+        HIP_OR_FAIL(hipEventRecord(s->lev[2 * j + 1], qs[k]));
+    }
+    for (int k = 1; k < nset; ++k) {   // join
+        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[k], qs[k]));
+        HIP_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[k], 0));
+    }
+    HIP_OR_FAIL(hipEventRecord(s->ev[2], st));   // end of the trace phase
+    HIP_OR_FAIL(hipEventSynchronize(s->ev[2]));
+    double trace_ms = 0.0, kernel_ms = 0.0;
     int launches = 0;
-    for (int done = 0; done < p->spp && bh > 0; done += chunk) {
-        a.samples = std::min(chunk, p->spp - done);
-        HIP_OR_FAIL(hipEventRecord(s->ev[2], st));
-        HIP_OR_FAIL(tpt::launch_trace(a, st));
-        HIP_OR_FAIL(hipEventRecord(s->ev[3], st));
-        HIP_OR_FAIL(hipEventSynchronize(s->ev[3]));
+    {
         float ms = 0.0f;
-        HIP_OR_FAIL(hipEventElapsedTime(&ms, s->ev[2], s->ev[3]));
-        trace_ms += ms;
-        ++launches;
+        HIP_OR_FAIL(hipEventElapsedTime(&ms, s->ev[1], s->ev[2]));
+        trace_ms = ms;   // wall time of the trace phase (overlapping launches counted once)
+        for (size_t j = 0; j < plan.size(); ++j) {
+            if (set_bh[plan[j].set] <= 0) continue;
+            HIP_OR_FAIL(hipEventElapsedTime(&ms, s->lev[2 * j], s->lev[2 * j + 1]));
+            kernel_ms += ms;
+            ++launches;
+        }
     }
 
     // copyToFB (:553) + radiance readout, per frame
@@ -727,6 +848,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         (void)hipEventElapsedTime(&ms, s->ev[0], s->ev[1]);
         stats->rng_init_ms = ms;
         stats->trace_ms = trace_ms;
+        stats->trace_kernel_ms = kernel_ms;
         (void)hipEventElapsedTime(&ms, s->ev[2], s->ev[3]);
         stats->resolve_ms = ms;
         stats->trace_launches = launches;
