@@ -52,12 +52,6 @@
 #ifndef TPT_LDS_NODES_MAX
 #define TPT_LDS_NODES_MAX 0
 #endif
-#ifndef TPT_PRIO
-#define TPT_PRIO 0        // 1: wave issue priority from its rays per sample (experiment)
-#endif
-#ifndef TPT_PRIO_STEP
-#define TPT_PRIO_STEP 3   // rays per sample per priority level
-#endif
 #ifndef TPT_TRACE_WAVES
 #define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator
 #endif
@@ -952,21 +946,6 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             TPT_SEC(6)
         }
         if (__ballot(ts != TS_DEAD) == 0ull) break;
-#if TPT_PRIO
-        {
-            // issue priority by the wave's rays per sample so far (its first live
-            // lane's; the lanes of a wave are balanced): the heaviest waves are the
-            // launch's critical chains, the light ones fill the slots around them
-            const int done_s = a.samples - remaining;
-            const int lead = __builtin_amdgcn_readfirstlane((int)c_trav);
-            const int lead_s = __builtin_amdgcn_readfirstlane(done_s > 0 ? done_s : 1);
-            const int rps = lead / lead_s;
-            if (rps >= 3 * TPT_PRIO_STEP) __builtin_amdgcn_s_setprio(3);
-            else if (rps >= 2 * TPT_PRIO_STEP) __builtin_amdgcn_s_setprio(2);
-            else if (rps >= TPT_PRIO_STEP) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
 #ifdef TPT_PROFILE_PHASES
         t_loop0 = wall_clock64();
         p_done += t_loop0 - t_iter0;
