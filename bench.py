@@ -275,11 +275,15 @@ def main():
         bytes_total = (B_INNER * l_tot["internal_visits"] + B_WIDE * l_tot["wide_visits"] + B_LEAF * l_tot["leaf_tests"] +
                        B_HIT * l_tot["shade_hits"] + B_PIX * l_tot["pixels"])
         bytes_per_launch = bytes_total / nl
-        # each launch's own duration (HIP events on its stream; what rocprofv3
-        # reports per kernel): the launch pipeline overlaps launches, so their
-        # sum exceeds the trace phase's wall time and this rate is conservative
+        # avg_launch_s: each launch's own duration (HIP events on its stream;
+        # what rocprofv3 reports per kernel dispatch).  The launch pipeline runs
+        # launches of different band sets concurrently (concurrency = summed
+        # launch time / trace-phase wall time), so the kernel's byte rate is
+        # bytes per launch / (launch duration / concurrency) -- the algorithmic
+        # bytes of the trace phase over its wall time
         avg_launch_s = (l_tot["trace_kernel_ms"] / nl) / 1e3
-        achieved = bytes_per_launch / avg_launch_s / 1e9
+        concurrency = l_tot["trace_kernel_ms"] / max(l_tot["trace_ms"], 1e-9)
+        achieved = bytes_per_launch * concurrency / avg_launch_s / 1e9
         traffic = None
         batch = (f" x {n_frames} frames (seeds {seeds[0]}..{seeds[-1]}), each banded across {ranks} ranks"
                  if n_frames > 1 else "")
@@ -325,6 +329,7 @@ def main():
                          "traffic": traffic,
                          "kernel": "k_trace", "bytes_per_launch": bytes_per_launch,
                          "avg_launch_ms": round(avg_launch_s * 1e3, 3),
+                         "concurrency": round(concurrency, 3),
                          "launches_per_step": nl / K},
             "phases_ms_per_step": {"rng_init": round(l_tot["rng_init_ms"] / K, 3),
                                    "trace": round(l_tot["trace_ms"] / K, 3),

@@ -56,6 +56,8 @@ try:
                 s["launches_per_step"] = b.get("roofline", {}).get("launches_per_step")
 except OSError:
     pass
-if p.get("GRBM_GUI_ACTIVE") and s.get("avg_duration_ms"):
+# (launches that overlap each other -- the launch pipeline -- make the traced
+# durations longer than the GPU-busy time of one dispatch: no clock estimate)
+if p.get("GRBM_GUI_ACTIVE") and s.get("avg_duration_ms") and (s.get("launches_per_step") or 1) <= 1:
     s["effective_clock_ghz"] = p["GRBM_GUI_ACTIVE"] / 8.0 / (s["avg_duration_ms"] * 1e6)
 print(json.dumps(s, indent=1))
