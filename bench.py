@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--spp-per-launch", type=int, default=0)
     ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
     ap.add_argument("--refill", type=int, default=0, help="0 = library default")
+    ap.add_argument("--extra-streams", type=int, default=0,
+                    help="diagnostic: create this many busy-once HIP streams before the scene (as a process "
+                         "group's communicator streams would), to check the launch pipeline's queue use")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port on rank 0 at N=1")
     ap.add_argument("--cpu-spp", type=int, default=16)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -180,6 +183,12 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    extra = []
+    for _ in range(args.extra_streams):
+        q = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(q):
+            extra.append(torch.ones(1024, device=f"cuda:{dev}") * 2.0)
+    torch.cuda.synchronize()
     scene = T.Scene(scene_file(args.scene))
     d_scene = scene.copySceneToDevice(dev)
     t0 = time.perf_counter()

@@ -217,12 +217,20 @@ struct tpt_scene {
         if (stream) (void)hipStreamDestroy(stream);
     }
 
-    // streams for sets 1..n-1 and the fork/join events
+    // streams for the n band sets and the fork/join events.  Every set needs a
+    // hardware queue of its own: two streams on one queue run their launches
+    // one after another (a process has GPU_MAX_HW_QUEUES = 4; measured on the
+    // box, one or two idle streams created earlier in the process -- a
+    // communicator's -- made two sets share a queue: -25 %).  The runtime
+    // keeps a queue pool per stream priority, so the sets' streams are created
+    // at the greatest priority, where nothing else in the process competes.
     hipError_t ensure_pipe(int n) {
         hipError_t e = hipSuccess;
-        while (e == hipSuccess && (int)pipe.size() < n - 1) {
+        int lo = 0, hi = 0;
+        if (!std::getenv("TPT_PIPE_NORMAL_PRIO")) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        while (e == hipSuccess && (int)pipe.size() < n) {
             hipStream_t q = nullptr;
-            e = hipStreamCreateWithFlags(&q, hipStreamNonBlocking);
+            e = hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi);
             if (e == hipSuccess) pipe.push_back(q);
         }
         for (int i = 0; e == hipSuccess && i < 2 * kMaxPipe; ++i)
@@ -715,8 +723,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     if (nset > 1) {
         HIP_OR_FAIL(s->ensure_pipe(nset));
         HIP_OR_FAIL(hipEventRecord(s->pipe_ev[0], st));   // fork: RNG init and the sums' reset are done
-        for (int k = 1; k < nset; ++k) {
-            qs[k] = s->pipe[k - 1];
+        for (int k = 0; k < nset; ++k) {
+            qs[k] = s->pipe[k];
             HIP_OR_FAIL(hipStreamWaitEvent(qs[k], s->pipe_ev[0], 0));
         }
     }
@@ -753,9 +761,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         HIP_OR_FAIL(tpt::launch_trace(ak, qs[k]));
         HIP_OR_FAIL(hipEventRecord(s->lev[2 * j + 1], qs[k]));
     }
-    for (int k = 1; k < nset; ++k) {   // join
-        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[k], qs[k]));
-        HIP_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[k], 0));
+    for (int k = 0; nset > 1 && k < nset; ++k) {   // join
+        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[1 + k], qs[k]));
+        HIP_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[1 + k], 0));
     }
     HIP_OR_FAIL(hipEventRecord(s->ev[2], st));   // end of the trace phase
     HIP_OR_FAIL(hipEventSynchronize(s->ev[2]));
