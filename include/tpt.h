@@ -93,6 +93,15 @@ typedef struct {
     int32_t spp_per_launch;       /* 0 = auto; chunks the spp loop over launches */
     int32_t flags;                /* TPT_FLAG_* */
     int32_t refill;               /* 0 = auto: lanes (of 64) below which a wave stops to shade */
+    /* Launch pipeline.  pipe_sets: 0 = auto (3 interleaved band sets
+     * from 1024 spp, else 1), 1 = one stream, 2..4 = that many sets (from 256 spp);
+     * pipe_chunks: spp chunks per set, 0 = auto (8).  Every schedule is bit-identical
+     * to one launch.  The sets run on library-owned streams created at the device's
+     * greatest stream priority: HIP gives each priority its own pool of hardware queues
+     * (GPU_MAX_HW_QUEUES, 4 by default), and two sets whose streams share a queue run
+     * one after the other (-25 % measured).  A host application that issues its own
+     * greatest-priority work on the device while tpt_render runs shares those queues. */
+    int32_t pipe_sets, pipe_chunks;
 } tpt_params;
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
@@ -185,9 +194,21 @@ tpt_status tpt_scene_read_world(tpt_scene* scene, float* wverts, float* wnorms);
 /* Per-pixel RNG states after setupRandSeed for the first n pixels: 6 words
  * each {v0..v4, d}. */
 tpt_status tpt_debug_rng_init(int device, uint64_t seed, uint64_t first_pixel, uint32_t n, uint32_t* states);
-/* Trace n rays (origins/dirs xyz) against the built BVH: hit fid (-1 miss), t, u, v. */
+/* Trace n rays (origins/dirs xyz) against the built BVH: hit fid (-1 miss), t, u, v.
+ * mode 0: closest hit in the reference's visit order (traverseBVH, path_tracer.cu:61-107);
+ * 1: closest hit through the render's traversal (nearer-first, culled, 4-wide);
+ * 2: any hit (shadow rays); 3: the render's two-pass direct probe -- hit = the
+ * closest hit if it is an emitter, -2 if a non-emitter is closer, -1 if no emitter is hit. */
 tpt_status tpt_debug_trace_rays(tpt_scene* scene, uint32_t n, const float* origins, const float* dirs,
-                                int32_t* hit, float* t, float* uv);
+                                int32_t mode, int32_t* hit, float* t, float* uv);
+/* Known-answer evaluation of the trace kernel's own device functions, one case
+ * per lane (tests pin them to the reference's headers):
+ *   op 0 rayHitBBox   in 12/case (o3 d3 min3 max3)          out 2 (box_hit, min/max verdict)
+ *   op 1 rayHitTriangle in 15 (o3 d3 v0_3 v1_3 v2_3)         out 4 (hit, dist, u, v)
+ *   op 2 DeltaLight::sample in 16 (type color3 intensity pos3 dir3 cos_outer
+ *        inv_cos_cone_diff p3)                              out 6 (dir3, radiance3)
+ *   op 3 Spectrum::toUChar in 3                             out 3 (bytes as floats) */
+tpt_status tpt_debug_hot_kat(int device, int32_t op, uint32_t n, const float* in, float* out);
 /* Host-only: the SAH 4-wide traversal tree tpt_scene_build uploads, over n >= 2
  * leaf boxes (6 floats each, by LBVH sorted position) and emitter flags.  Writes
  * at most `cap` nodes of 32 floats (inner4 layout, device_api.hpp) and the

@@ -575,6 +575,14 @@ static inline float new_direction(v3 d, v3 n, const orc_material* m, uint32_t st
     }
 }
 
+/* CalcDistAttenuation (delta_light.h:25-33) */
+static inline v3 dist_atten(float dist, v3 rad) {
+    float d2 = dist * dist;
+    float att = 1.0f / (d2 + 1.0f);
+    att *= fsq(fsat(1.0f - fsq(d2 * 0.01f)));
+    return vscale(att, rad);
+}
+
 /* DeltaLight::sample + CalcDistAttenuation (delta_light.h:25-33, 35-130) */
 static inline void light_sample(const orc_light* L, v3 p, v3* dir, v3* rad) {
     v3 color = V3(L->color[0], L->color[1], L->color[2]);
@@ -598,10 +606,7 @@ static inline void light_sample(const orc_light* L, v3 p, v3* dir, v3* rad) {
         float fall = fsq(fsat(cos_t - L->cos_outer) * L->inv_cos_cone_diff);
         *rad = vscale(fall, vscale(L->intensity, color));
     }
-    float d2 = dist * dist;
-    float att = 1.0f / (d2 + 1.0f);
-    att *= fsq(fsat(1.0f - fsq(d2 * 0.01f)));
-    *rad = vscale(att, *rad);
+    *rad = dist_atten(dist, *rad);
 }
 
 /* sampleEnvLights (:288-294) + Vec2UV (env_light.cuh:72-78) + point/clamp
@@ -946,3 +951,42 @@ int orc_render(const orc_scene* s, const orc_env* env, const orc_camera* cam, co
     free(is_tab.w); free(is_tab.cond); free(is_tab.row); free(is_tab.marg);
     return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* KAT entry points: the hot-path functions one at a time, pinned against the */
+/* reference's own headers compiled here (oracle/_ref/ref_hot_kat,           */
+/* tests/golden/ref_hot_kat.json).                                           */
+/* ------------------------------------------------------------------------ */
+int orc_kat_box_hit(const float o[3], const float d[3], const float bmin[3], const float bmax[3]) {
+    ray_t r;
+    r.o = V3(o[0], o[1], o[2]);
+    r.d = V3(d[0], d[1], d[2]);
+    return hit_box(&r, bmin, bmax);
+}
+
+int orc_kat_tri(const float o[3], const float d[3], const float v0[3], const float v1[3], const float v2[3],
+                float out[3]) {
+    ray_t r;
+    r.o = V3(o[0], o[1], o[2]);
+    r.d = V3(d[0], d[1], d[2]);
+    return hit_tri(&r, V3(v0[0], v0[1], v0[2]), V3(v1[0], v1[1], v1[2]), V3(v2[0], v2[1], v2[2]), &out[0], &out[1],
+                   &out[2]);
+}
+
+void orc_kat_light(const orc_light* L, const float p[3], float dir[3], float rad[3]) {
+    v3 dd, rr;
+    light_sample(L, V3(p[0], p[1], p[2]), &dd, &rr);
+    dir[0] = dd.x; dir[1] = dd.y; dir[2] = dd.z;
+    rad[0] = rr.x; rad[1] = rr.y; rad[2] = rr.z;
+}
+
+void orc_kat_dist_atten(float dist, float rgb[3]) {
+    v3 r = dist_atten(dist, V3(rgb[0], rgb[1], rgb[2]));
+    rgb[0] = r.x; rgb[1] = r.y; rgb[2] = r.z;
+}
+
+void orc_kat_to_uchar(const float rgb[3], uint8_t out[3]) {
+    for (int i = 0; i < 3; ++i) out[i] = to_uchar(rgb[i]);
+}
+
+void orc_kat_default_material(orc_material* m) { *m = k_default_material; }

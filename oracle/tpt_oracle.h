@@ -129,6 +129,19 @@ int orc_trace_ray(const orc_node* nodes, uint32_t n_faces, const float* wverts,
                   const uint32_t* indices, const float o[3], const float d[3],
                   float* t_out, float uv_out[2]);
 
+/* KAT entry points (tests/test_oracle_pinned.py vs tests/golden/ref_hot_kat.json):
+ * rayHitBBox (geometry_queries.h:18-46); rayHitTriangle (:65-86), out = dist, u, v
+ * (written only on a hit); DeltaLight::sample (delta_light.h:105-130);
+ * CalcDistAttenuation (:25-33), rgb in place; Spectrum::toUChar (material.h:74-81);
+ * Material() (material.h:88-103). */
+int orc_kat_box_hit(const float o[3], const float d[3], const float bmin[3], const float bmax[3]);
+int orc_kat_tri(const float o[3], const float d[3], const float v0[3], const float v1[3], const float v2[3],
+                float out[3]);
+void orc_kat_light(const orc_light* L, const float p[3], float dir[3], float rad[3]);
+void orc_kat_dist_atten(float dist, float rgb[3]);
+void orc_kat_to_uchar(const float rgb[3], uint8_t out[3]);
+void orc_kat_default_material(orc_material* m);
+
 float orc_parity_sinf(float x);
 float orc_parity_cosf(float x);
 /* trig_mode 1 sin/cos of phi in [0, 2pi] (identical to the HIP kernel) */

@@ -125,7 +125,7 @@ def image_metrics(a, b):
                 bit_same=float(bit_same))
 
 
-def assert_parity(m, bit_min=0.95):
+def assert_parity(m, bit_min=1.0):
     assert m["mean"] <= 1e-3, m
     assert m["p99"] <= 1e-2, m
     assert m["within1"] >= 0.995, m
@@ -163,8 +163,8 @@ def test_render_parity(built, name, W, H, spp, depth, env, order):
     orad, obgra, oc = O.render(o, W, H, spp, depth, 42, env=sky[::-1].copy() if env else None, trig_mode=1)
     m = image_metrics(rad, orad)
     assert_parity(m)
-    # copyToFB layout: flipped rows, B,G,R bytes; alpha untouched
-    assert (np.abs(fb[..., :3].astype(int) - obgra[..., :3].astype(int)) <= 1).mean() >= 0.995
+    # copyToFB layout: flipped rows, B,G,R bytes (exact); alpha untouched
+    assert np.array_equal(fb[..., :3], obgra[..., :3])
     assert (fb[..., 3] == 0).all()
     # ray counts are deterministic; equal unless a diverged path took a different branch
     assert abs(stats["traversals"] - oc["traversals"]) <= 0.01 * oc["traversals"]
@@ -180,6 +180,44 @@ def test_render_parity(built, name, W, H, spp, depth, env, order):
             # one even-depth binary node the reference also pops
             assert stats["internal_visits"] + stats["wide_visits"] <= oc["internal_visits"]
             assert stats["leaf_tests"] <= oc["leaf_tests"]
+
+
+# The BASELINE configurations at their full resolution and a few
+# spp: C2 box, C3 ball + sky (2048x1024 procedural equirect), C4 tir at depth
+# 32, C5 the 131,712-triangle merge at 3840x2160.  The oracle runs on the
+# box's host cores (OpenMP); the GPU renders in the default order, in the
+# reference's order and (C2) through a forced launch pipeline.
+FULL = [
+    # name, W, H, spp, depth, env
+    ("box", 1920, 1080, 2, 8, None),
+    ("ball", 1920, 1080, 2, 8, "sky"),
+    ("tir", 1920, 1080, 2, 32, None),
+    ("c5", 3840, 2160, 1, 8, None),
+]
+
+
+@pytest.mark.parametrize("name,W,H,spp,depth,env", FULL)
+def test_render_parity_full_resolution(built, name, W, H, spp, depth, env):
+    s, d, o = built[name]
+    sky = T.procedural_sky(2048, 1024) if env else None
+    orad, obgra, oc = O.render(o, W, H, spp, depth, 42, env=sky[::-1].copy() if env else None, trig_mode=1)
+    pt = T.PathTracer("", W, H, 0)
+    if env:
+        pt.envLight = T.EnvLight(sky, 0)
+    runs = [("ordered", {}), ("reference", {"flags": T._lib.FLAG_REF_ORDER})]
+    if name == "box":   # 3 band sets on 3 streams, 2 chunks each (host/api.cpp launch pipeline)
+        runs.append(("pipeline", {"pipe_sets": 3, "pipe_chunks": 2}))
+    for label, kw in runs:
+        fb = np.zeros((H, W, 4), np.uint8)
+        rad = np.zeros((H, W, 3), np.float32)
+        st = pt.doTrace(d, s.m_camera, fb, spp, seed=42, max_depth=depth, radiance=rad, **kw)
+        m = image_metrics(rad, orad)
+        assert m["bit_same"] == 1.0, (label, m, int((rad.view(np.uint32) != orad.view(np.uint32)).any(-1).sum()))
+        assert np.array_equal(fb[..., :3], obgra[..., :3]), label
+        assert st["traversals"] == oc["traversals"], label
+        assert st["shade_hits"] == oc["shade_hits"], label
+        if label == "pipeline":
+            assert st["trace_launches"] > 3
 
 
 @pytest.mark.parametrize("name", ["ball", "box1", "box"])
@@ -269,39 +307,40 @@ def test_spp_chunking_bit_identical(built):
     assert np.array_equal(_bits(a), _bits(b))
 
 
-def test_launch_pipeline_bit_identical(built, monkeypatch):
+def test_launch_pipeline_bit_identical(built):
     """The launch pipeline (row band sets on their own streams, spp in offset
-    chunks, host/api.cpp; the default from 1024 spp on, TPT_PIPE forces it from
-    256) equals one launch bit for bit: 2, 3 and 4 sets, banded across ranks,
-    and a frame batch."""
+    chunks, host/api.cpp; the default from 1024 spp on, tpt_params.pipe_sets
+    forces it from 256) equals one launch bit for bit: 2, 3 and 4 sets, banded
+    across ranks, and a frame batch."""
     s, d, _ = built["box"]
     W, H, spp = 96, 80, 256
     pt = T.PathTracer("", W, H, 0)
-    monkeypatch.setenv("TPT_PIPE", "1")
     one = np.zeros((H, W, 3), np.float32)
     fb1 = np.zeros((H, W, 4), np.uint8)
-    st1 = pt.doTrace(d, s.m_camera, fb1, spp, seed=11, radiance=one)
+    st1 = pt.doTrace(d, s.m_camera, fb1, spp, seed=11, radiance=one, pipe_sets=1)
     assert st1["trace_launches"] == 1
     seeds = [11, 12]
     batch1 = [np.zeros((H, W, 3), np.float32) for _ in seeds]
-    pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch1)
+    pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch1, pipe_sets=1)
     for sets, launches in ((2, 5), (3, 8), (4, 11)):   # chunks of 128 spp, set k k/sets of a chunk ahead
-        monkeypatch.setenv("TPT_PIPE", str(sets))
         got = np.zeros((H, W, 3), np.float32)
         fb = np.zeros((H, W, 4), np.uint8)
-        st = pt.doTrace(d, s.m_camera, fb, spp, seed=11, radiance=got)
+        st = pt.doTrace(d, s.m_camera, fb, spp, seed=11, radiance=got, pipe_sets=sets)
         assert st["trace_launches"] == launches, sets
         assert st["traversals"] == st1["traversals"]
         assert st["trace_kernel_ms"] > 0.0
         assert np.array_equal(_bits(got), _bits(one)), sets
         assert np.array_equal(fb, fb1), sets
-    monkeypatch.setenv("TPT_PIPE", "2")
+    # more chunks per set: 3 sets x 2 chunks of >= 128 spp
+    got = np.zeros((H, W, 3), np.float32)
+    st = pt.doTrace(d, s.m_camera, None, spp, seed=11, radiance=got, pipe_sets=3, pipe_chunks=2)
+    assert np.array_equal(_bits(got), _bits(one))
     banded = np.zeros((H, W, 3), np.float32)
     for idx in range(2):
-        pt.doTrace(d, s.m_camera, None, spp, seed=11, radiance=banded, band=(16, 2, idx))
+        pt.doTrace(d, s.m_camera, None, spp, seed=11, radiance=banded, band=(16, 2, idx), pipe_sets=2)
     assert np.array_equal(_bits(banded), _bits(one))
     batch = [np.zeros((H, W, 3), np.float32) for _ in seeds]
-    st = pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch)
+    st = pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch, pipe_sets=2)
     assert st["trace_launches"] > 1
     for f in range(len(seeds)):
         assert np.array_equal(_bits(batch[f]), _bits(batch1[f])), f

@@ -156,14 +156,16 @@ class DeviceScene:
         check(lib().tpt_scene_read_world(self.handle, _ptr(wv), _ptr(wn)))
         return wv, wn
 
-    def trace_rays(self, origins, dirs):
+    def trace_rays(self, origins, dirs, mode=0):
+        """mode 0: the reference's visit order; 1: the render's ordered culled
+        traversal; 2: any hit; 3: two-pass probe (see tpt_debug_trace_rays)."""
         o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
         n = len(o)
         hit = np.zeros(n, np.int32)
         t = np.zeros(n, np.float32)
         uv = np.zeros((n, 2), np.float32)
-        check(lib().tpt_debug_trace_rays(self.handle, n, _ptr(o), _ptr(d), _ptr(hit), _ptr(t), _ptr(uv)))
+        check(lib().tpt_debug_trace_rays(self.handle, n, _ptr(o), _ptr(d), mode, _ptr(hit), _ptr(t), _ptr(uv)))
         return hit, t, uv
 
     def close(self):
@@ -176,6 +178,17 @@ class DeviceScene:
             self.close()
         except Exception:
             pass
+
+
+def hot_kat(op, cases, device=0):
+    """The trace kernel's own device functions on `cases` (tpt_debug_hot_kat):
+    op 0 box (n,12) -> (n,2); 1 triangle (n,15) -> (n,4); 2 light (n,16) -> (n,6);
+    3 toUChar (n,3) -> (n,3).  Tests pin them to the reference's headers."""
+    nin, nout = {0: (12, 2), 1: (15, 4), 2: (16, 6), 3: (3, 3)}[op]
+    a = np.ascontiguousarray(cases, np.float32).reshape(-1, nin)
+    out = np.zeros((len(a), nout), np.float32)
+    check(lib().tpt_debug_hot_kat(device, op, len(a), _ptr(a), _ptr(out)))
+    return out
 
 
 class BVH:
@@ -298,7 +311,8 @@ class PathTracer:
 
     def doTrace(self, d_scene: DeviceScene, camera: Camera, framebuffer=None, nSamplesPerPixel: int = 64,
                 seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
-                flags: int = 0, refill: int = 0, accumulate: bool = False):
+                flags: int = 0, refill: int = 0, accumulate: bool = False, pipe_sets: int = 0,
+                pipe_chunks: int = 0):
         """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
         or torch CUDA tensors / raw device pointers (device, int).
         accumulate=True: progressive rendering (TPT_FLAG_ACCUMULATE) -- continue
@@ -315,7 +329,7 @@ class PathTracer:
             seed = int(time.time())
         self._last_seed = seed
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags,
-                        refill)
+                        refill, pipe_sets, pipe_chunks)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
         rad_p = _addr(radiance)
@@ -326,7 +340,8 @@ class PathTracer:
 
     def doTraceFrames(self, d_scene: DeviceScene, camera: Camera, seeds, framebuffers=None,
                       nSamplesPerPixel: int = 64, max_depth: int = 8, radiances=None, band=(16, 1, 0),
-                      spp_per_launch: int = 0, flags: int = 0, refill: int = 0, accumulate: bool = False):
+                      spp_per_launch: int = 0, flags: int = 0, refill: int = 0, accumulate: bool = False,
+                      pipe_sets: int = 0, pipe_chunks: int = 0):
         """A batch of independent frames in one trace launch (tpt_render_frames):
         frame f is doTrace(..., seed=seeds[f]) bit for bit.  framebuffers /
         radiances: None or one buffer (or None) per frame."""
@@ -340,7 +355,7 @@ class PathTracer:
             flags |= _lib.FLAG_ACCUMULATE
         W, H = self.m_width, self.m_height
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seeds[0], band[0], band[1], band[2], spp_per_launch,
-                        flags, refill)
+                        flags, refill, pipe_sets, pipe_chunks)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
 

@@ -55,7 +55,7 @@ class Params(C.Structure):
     _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_int32), ("max_depth", C.c_int32),
                 ("seed", C.c_uint64), ("band_rows", C.c_int32), ("band_count", C.c_int32),
                 ("band_index", C.c_int32), ("spp_per_launch", C.c_int32), ("flags", C.c_int32),
-                ("refill", C.c_int32)]
+                ("refill", C.c_int32), ("pipe_sets", C.c_int32), ("pipe_chunks", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -91,8 +91,9 @@ SIGNATURES = [
     ("tpt_scene_read_bvh", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_scene_read_world", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_debug_rng_init", C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]),
-    ("tpt_debug_trace_rays", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                       C.c_void_p]),
+    ("tpt_debug_trace_rays", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
+                                       C.c_void_p, C.c_void_p]),
+    ("tpt_debug_hot_kat", C.c_int, [C.c_int, C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("tpt_wide_tree_build", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                         C.POINTER(C.c_int32)]),
     ("tpt_gltf_load", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),

@@ -165,7 +165,9 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s);
 // trace.hip
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
-hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int32_t* hit,
+// KAT kernel over the trace kernel's device functions (tpt_debug_hot_kat)
+hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipStream_t s);
+hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int mode, int32_t* hit,
                              float* t, float* uv, hipStream_t s);
 
 }  // namespace tpt

@@ -227,7 +227,7 @@ struct tpt_scene {
     hipError_t ensure_pipe(int n) {
         hipError_t e = hipSuccess;
         int lo = 0, hi = 0;
-        if (!std::getenv("TPT_PIPE_NORMAL_PRIO")) e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        e = hipDeviceGetStreamPriorityRange(&lo, &hi);
         while (e == hipSuccess && (int)pipe.size() < n) {
             hipStream_t q = nullptr;
             e = hipStreamCreateWithPriority(&q, hipStreamNonBlocking, hi);
@@ -424,7 +424,6 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     const uint32_t td = b.out_max_depth;
     uint32_t wide_need = 3 * ((td + 1) / 2) + 1;
     s->wide_tree = 0;
-    const char* wt = std::getenv("TPT_WIDE_TREE");   // "lbvh": keep the even-depth view (A/B runs)
     s->emit_root = -1;
     s->emit_inline = 0;
     if (n > 1 && s->boxes_finite) {
@@ -435,10 +434,17 @@ tpt_status tpt_scene_build(tpt_scene* s) {
         HIP_OR_FAIL(hipMemcpyAsync(lemit.data(), s->emit.p + (n - 1), n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    s->stream));
         HIP_OR_FAIL(hipStreamSynchronize(s->stream));
-        tpt::WideParams prm;   // tuning override for A/B runs
-        if (const char* v = std::getenv("TPT_WIDE_SWEEP")) prm.sweep_max = std::atoi(v);
+        tpt::WideParams prm;
+#ifdef TPT_WIDE_SWEEP
+        prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
+#endif
         const int leaf_base = (int)n - 1;
-        if (!(wt && std::strcmp(wt, "lbvh") == 0)) {
+#ifdef TPT_WIDE_TREE_LBVH
+        const bool sah = false;   // A/B builds: keep the LBVH's even-depth view
+#else
+        const bool sah = true;
+#endif
+        if (sah) {
             // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
             std::vector<int> all(n);
             for (size_t p = 0; p < n; ++p) all[p] = (int)p;
@@ -567,7 +573,11 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.boxes_finite = s->boxes_finite;
     a.any_emitter = s->any_emitter;
     a.emit_root = s->emit_root;
-    a.emit_inline = std::getenv("TPT_NO_EMIT_INLINE") ? 0 : s->emit_inline;   // env: A/B runs
+#ifdef TPT_NO_EMIT_INLINE
+    a.emit_inline = 0;   // A/B builds: probe pass 1 as a traversal always
+#else
+    a.emit_inline = s->emit_inline;
+#endif
     a.env = env ? env->texels.p : nullptr;
     a.env_w = env ? env->w : 0;
     a.env_h = env ? env->h : 0;
@@ -673,7 +683,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // launch is mid-flight and takes the freed slots.  A pixel's samples still
     // run in order (its set's launches are stream-ordered, RNG and sums persist
     // between chunks), so the result is bit-identical to one launch.
-    // TPT_PIPE=<P> (1: one stream), TPT_PIPE_CHUNKS=<chunks per set> override;
+    // params pipe_sets (1: one stream) and pipe_chunks (chunks per set) override;
     // an explicit spp_per_launch keeps the single-stream chunked loop.
     int chunk = p->spp_per_launch;
     int nset = 1;
@@ -681,10 +691,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         // one stream: chunk only past ~4096 spp of 1080p pixels so one launch stays below ~5 s
         const double band_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
         chunk = (int)std::max(1.0, std::floor(4096.0 * 2073600.0 / band_pix));
-        const char* pe = std::getenv("TPT_PIPE");
-        const char* pc = std::getenv("TPT_PIPE_CHUNKS");
-        nset = pe ? std::atoi(pe) : 3;
-        const int per_set = std::max(pc ? std::atoi(pc) : 8, 1);
+        const bool forced = p->pipe_sets > 0;
+        nset = forced ? p->pipe_sets : 3;
+        const int per_set = p->pipe_chunks > 0 ? p->pipe_chunks : 8;
         nset = std::max(1, std::min(nset, kMaxPipe));
         // worth it only with several chunks of real work and rows for every set
         if (bh < nset * band_rows) nset = 1;
@@ -692,8 +701,12 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         // (measured on box 1080p, 3 sets: 1024 spp +6.7 %; 256 spp -2 %, 32-spp
         // chunks -4 %: concurrently running launches at different rows cost
         // locality, and every launch its prologue)
-        if (nset > 1) chunk = std::min(chunk, std::max(kPipeMinChunk, (p->spp + per_set - 1) / per_set));
-        if (p->spp < (pe ? 2 : 8) * kPipeMinChunk) nset = 1;
+        // (both pipe_sets and pipe_chunks given: exactly that schedule, any chunk
+        // size -- tests run the pipeline at full resolution and a few spp)
+        const bool exact = forced && p->pipe_chunks > 0;
+        const int min_chunk = exact ? 1 : kPipeMinChunk;
+        if (nset > 1) chunk = std::min(chunk, std::max(min_chunk, (p->spp + per_set - 1) / per_set));
+        if (!exact && p->spp < (forced ? 2 : 8) * kPipeMinChunk) nset = 1;
     }
     chunk = std::min(chunk, p->spp);
     struct Launch {
@@ -710,7 +723,11 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         }
     }
     a.debug_waves = nullptr;
-    const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");   // phase-profiling builds only
+#ifdef TPT_PROFILE_PHASES
+    const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");   // per-wave dump, phase-profiling builds only
+#else
+    const char* dbg_path = nullptr;
+#endif
     const size_t dbg_launch =
         8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 15) / 16) * nf;
     const size_t dbg_words = dbg_launch * std::max<size_t>(plan.size(), 1);   // one region per launch
@@ -837,11 +854,13 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
             std::fclose(f);
         }
     }
+#ifdef TPT_PROFILE_PHASES
     if (std::getenv("TPT_DEBUG_COUNTERS")) {   // raw kernel counters (TPT_PROFILE_PHASES builds: 6..15 phases, 16..22 shading-pass sections)
         std::fprintf(stderr, "tpt counters:");
         for (int i = 0; i < 32; ++i) std::fprintf(stderr, " %llu", cnt[i]);
         std::fprintf(stderr, "\n");
     }
+#endif
     if (stats) {
         std::memset(stats, 0, sizeof *stats);
         stats->traversals = cnt[0];
@@ -910,9 +929,10 @@ tpt_status tpt_debug_rng_init(int device, uint64_t seed, uint64_t first, uint32_
     return TPT_OK;
 }
 
-tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const float* d, int32_t* hit, float* t,
-                                float* uv) {
+tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const float* d, int32_t mode, int32_t* hit,
+                                float* t, float* uv) {
     if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
+    if (mode < 0 || mode > 3) return fail(TPT_ERR_INVALID_ARG, "unknown trace mode");
     if (n && (!o || !d || !hit || !t || !uv)) return fail(TPT_ERR_INVALID_ARG, "null argument");
     DeviceGuard g(s->device);
     DevBuf<float> dorg, ddir, dt, duv;
@@ -924,13 +944,30 @@ tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const 
     HIP_OR_FAIL(duv.alloc(2 * (size_t)n));
     tpt::TraceArgs a{};
     fill_trace_args(s, nullptr, nullptr, a);
-    HIP_OR_FAIL(tpt::launch_trace_rays(a, n, dorg.p, ddir.p, dhit.p, dt.p, duv.p, s->stream));
+    HIP_OR_FAIL(tpt::launch_trace_rays(a, n, dorg.p, ddir.p, mode, dhit.p, dt.p, duv.p, s->stream));
     HIP_OR_FAIL(hipStreamSynchronize(s->stream));
     if (n) {
         HIP_OR_FAIL(hipMemcpy(hit, dhit.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
         HIP_OR_FAIL(hipMemcpy(t, dt.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
         HIP_OR_FAIL(hipMemcpy(uv, duv.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
     }
+    return TPT_OK;
+}
+
+tpt_status tpt_debug_hot_kat(int device, int32_t op, uint32_t n, const float* in, float* out) {
+    static const int kIn[4] = {12, 15, 16, 3}, kOut[4] = {2, 4, 6, 3};
+    if (op < 0 || op > 3) return fail(TPT_ERR_INVALID_ARG, "unknown KAT op");
+    if (n && (!in || !out)) return fail(TPT_ERR_INVALID_ARG, "null argument");
+    int ndev = tpt_device_count();
+    if (ndev <= 0) return fail(TPT_ERR_NO_DEVICE, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(TPT_ERR_INVALID_ARG, "bad device index");
+    DeviceGuard g(device);
+    DevBuf<float> din, dout;
+    HIP_OR_FAIL(din.upload(in, (size_t)kIn[op] * n, nullptr));
+    HIP_OR_FAIL(dout.alloc((size_t)kOut[op] * std::max(n, 1u)));
+    HIP_OR_FAIL(tpt::launch_hot_kat(op, n, din.p, dout.p, nullptr));
+    HIP_OR_FAIL(hipDeviceSynchronize());
+    if (n) HIP_OR_FAIL(hipMemcpy(out, dout.p, sizeof(float) * kOut[op] * (size_t)n, hipMemcpyDeviceToHost));
     return TPT_OK;
 }
 

@@ -344,20 +344,28 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
 
 // rayHitTriangle (geometry_queries.h:65-86) on leaf position pos, e1/e2
 // pre-gathered.  Returns true when an any-hit ray may stop.
+// Moller-Trumbore core: rayHitTriangle's verdict (denom != 0, u, v >= 0,
+// u + v <= 1) and its dist/u/v, branch-free (t/u/v are computed either way).
+__device__ __forceinline__ bool tri_core(const V3& o, const V3& d, const V3& v0, const V3& e1, const V3& e2, float& t,
+                                         float& u, float& v) {
+    const V3 tv = o - v0;
+    const V3 p = cross(d, e2);
+    const V3 q = cross(tv, e1);
+    const float denom = dot(p, e1);
+    const float id = 1.0f / denom;
+    u = dot(p, tv) * id;
+    v = dot(q, d) * id;
+    t = dot(q, e2) * id;
+    return (denom != 0.0f) & !((u < 0.0f) | (v < 0.0f) | (u + v > 1.0f));
+}
+
 template <bool ORDERED>
 __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos) {
     const float4* tr = tri + 3 * pos;
     const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
     const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
-    const V3 tv = r.o - v0;
-    const V3 p = cross(r.d, e2);
-    const V3 q = cross(tv, e1);
-    const float denom = dot(p, e1);
-    const float id = 1.0f / denom;
-    const float u = dot(p, tv) * id;
-    const float v = dot(q, r.d) * id;
-    const float t = dot(q, e2) * id;
-    const bool inside = (denom != 0.0f) & !((u < 0.0f) | (v < 0.0f) | (u + v > 1.0f));
+    float t, u, v;
+    const bool inside = tri_core(r.o, r.d, v0, e1, e2, t, u, v);
     const bool better = ORDERED ? ((t < r.t) | ((t == r.t) & (r.hpos >= 0) & (pos > r.hpos))) : (t < r.t);
     const bool take = inside & better & (t > kDelta);   // :83
     r.t = take ? t : r.t;
@@ -391,38 +399,6 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
     if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint); }
     if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint); }
     if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint); }
-}
-
-// Returns false once the traversal has finished (or overflowed its stack).
-// The stack region holds stack_depth + 1 slots so the push below may write
-// unconditionally (a write at sp == stack_depth lands in the spare slot).
-template <bool ORDERED, typename StackT>
-__device__ __forceinline__ bool trav_step(Trav& r, const float4* __restrict__ inner, const float4* __restrict__ tri,
-                                          int nint, StackT* stk, int stack_depth, uint32_t& c_inner,
-                                          uint32_t& c_leaf, uint32_t& c_ovf) {
-    int next = -1;
-    bool push = false, stop = false;
-    int deferred = 0;
-    if (r.node < nint) {
-        ++c_inner;
-        inner_visit<ORDERED>(r, inner, next, push, deferred);
-    } else {
-        ++c_leaf;
-        stop = leaf_test<ORDERED>(r, tri, r.node - nint);
-    }
-    if (push) {
-        stk[r.sp * 256] = (StackT)deferred;
-        if (r.sp >= stack_depth) { ++c_ovf; return false; }
-        ++r.sp;
-    }
-    if (stop) return false;
-    if (next >= 0) {
-        r.node = next;
-        return true;
-    }
-    if (r.sp == 0) return false;
-    r.node = (int)stk[(--r.sp) * 256];
-    return true;
 }
 
 __device__ __forceinline__ V3 reflect_dir(V3 d, V3 n) { return d - (2.0f * dot(d, n)) * n; }   // :137-141
@@ -1075,6 +1051,9 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     }
 }
 
+// Spectrum::toUChar (material.h:74-81): truncating clamp to [0, 255]
+__device__ __forceinline__ uint8_t to_uchar(float c) { return (uint8_t)fclamp(c * 255.0f, 255.0f, 0.0f); }
+
 // copyToFB (path_tracer.cu:451-471) + the radiance readout (color / spp).
 __global__ void k_resolve(ResolveArgs a) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1095,30 +1074,148 @@ __global__ void k_resolve(ResolveArgs a) {
     }
     if (a.bgra) {   // Spectrum::toUChar (material.h:74-81): truncating clamp
         uint8_t* px = a.bgra + 4 * ((size_t)(a.height - y - 1) * (size_t)a.width + (size_t)x);
-        px[0] = (uint8_t)fclamp(b * 255.0f, 255.0f, 0.0f);
-        px[1] = (uint8_t)fclamp(g * 255.0f, 255.0f, 0.0f);
-        px[2] = (uint8_t)fclamp(r * 255.0f, 255.0f, 0.0f);
+        px[0] = to_uchar(b);
+        px[1] = to_uchar(g);
+        px[2] = to_uchar(r);
     }
 }
 
-// Closest hit for a batch of rays in the reference's visit order (tests).
+// A ray batch through one traversal (tests, tpt_debug_trace_rays):
+//  mode 0  closest hit in the reference's visit order (right-first DFS, no culling);
+//  mode 1  closest hit through the production traversal (nearer-first, culled,
+//          4-wide for finite rays), leaves tested as soon as they are reached;
+//  mode 2  any hit (shadow rays, TM_ANY);
+//  mode 3  direct probe in two passes (TM_EMIT, then TM_OCCL after an emitter
+//          hit): hit = the unbeaten emitter's fid, -2 when something beats it
+//          (the probe adds nothing), -1 when no emitter was hit.
+// Modes 1-3 run the same visit / cull / leaf functions as k_trace.
+constexpr int kRaysLdsSlots = 48;   // LDS stack slots per lane in k_trace_rays; deeper ones private
+
+template <bool ORDERED>
+__device__ __forceinline__ void trav_lane(Trav& r, const TraceArgs& a, LaneStack<int>& stk, uint32_t& c_ovf) {
+    const int nint = a.n_faces - 1;
+    while (r.node >= 0) {
+        if (r.node < nint) {
+            int next;
+            if (ORDERED && r.fin) {
+                next = inner_visit4(r, a.inner4, nullptr, 0, stk, r.sp);
+            } else {
+                int deferred;
+                bool push;
+                inner_visit<ORDERED>(r, a.inner, next, push, deferred);
+                stk.put(r.sp, deferred);
+                r.sp += push ? 1 : 0;
+            }
+            if (r.sp > a.stack_depth) {
+                ++c_ovf;
+                r.sp = 0;
+                next = -1;
+            }
+            r.node = next >= 0 ? next : (r.sp == 0 ? -1 : stk.get(--r.sp));
+        } else {
+            const bool stop = leaf_test<ORDERED>(r, a.tri, r.node - nint);
+            r.node = (stop || r.sp == 0) ? -1 : stk.get(--r.sp);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, const float* __restrict__ o,
-                                                    const float* __restrict__ d, int32_t* hit, float* t, float* uv) {
+                                                    const float* __restrict__ d, int mode, int32_t* hit, float* t,
+                                                    float* uv) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    uint32_t c0 = 0, c1 = 0, c2 = 0;
+    uint32_t c_ovf = 0;
     if (i < n) {
         Trav r;
-        trav_begin(r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
-                   TM_CLOSEST);
-        while (trav_step<false>(r, a.inner, a.tri, a.n_faces - 1, (int*)lds + threadIdx.x, a.stack_depth, c0, c1,
-                                c2)) {
+        const V3 ro = v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        LaneStack<int> stk;
+        stk.lds = (TPT_LDS int*)lds + threadIdx.x;
+        stk.nlds = kRaysLdsSlots;
+        int fid;
+        if (mode == 0) {
+            trav_begin(r, ro, rdir, TM_CLOSEST);   // binary nodes, the reference's ternary slab test
+            trav_lane<false>(r, a, stk, c_ovf);
+            fid = r.fid;
+        } else {
+            const int tm = mode == 1 ? TM_CLOSEST : (mode == 2 ? TM_ANY : TM_EMIT);
+            trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root);
+            trav_lane<true>(r, a, stk, c_ovf);
+            if (mode == 3 && r.mode == TM_EMIT && r.fid >= 0) {   // pass 2: does anything beat the emitter hit?
+                r.mode = TM_OCCL;
+                r.node = 0;
+                r.sp = 0;
+                trav_lane<true>(r, a, stk, c_ovf);
+            }
+            fid = (mode == 3 && r.mode == TM_OCCLUDED) ? -2 : r.fid;
         }
-        hit[i] = r.fid;
+        hit[i] = fid;
         t[i] = r.t;
         uv[2 * i] = r.u;
         uv[2 * i + 1] = r.v;
     }
+}
+
+// The kernel's own hot-path device functions, one case per lane, for the
+// known-answer tests against the reference's headers (tests only,
+// tpt_debug_hot_kat).  op 0: box_hit (rayHitBBox) with 1/dir hoisted as
+// trav_begin does, and the min/max form's verdict; op 1: tri_core on
+// (v0, v1 - v0, v2 - v0) as the scene pack stores them; op 2: light_sample;
+// op 3: to_uchar.  Layouts: see tpt.h.
+__global__ __launch_bounds__(256) void k_hot_kat(int op, uint32_t n, const float* __restrict__ in,
+                                                 float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    if (op == 0) {
+        const float* c = in + 12 * (size_t)i;
+        const V3 o = v3(c[0], c[1], c[2]), d = v3(c[3], c[4], c[5]);
+        const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        float t0, t1;
+        const bool h = box_hit(o, inv, c[6], c[7], c[8], c[9], c[10], c[11], t0, t1);
+        slab_minmax(o, inv, c[6], c[7], c[8], c[9], c[10], c[11], t0, t1);
+        out[2 * (size_t)i] = h ? 1.0f : 0.0f;
+        out[2 * (size_t)i + 1] = (fmaxf(t0, -kRealMax) <= fminf(t1, kRealMax)) ? 1.0f : 0.0f;
+    } else if (op == 1) {
+        const float* c = in + 15 * (size_t)i;
+        const V3 v0 = v3(c[6], c[7], c[8]);
+        const V3 e1 = v3(c[9], c[10], c[11]) - v0, e2 = v3(c[12], c[13], c[14]) - v0;
+        float t, u, v;
+        const bool h = tri_core(v3(c[0], c[1], c[2]), v3(c[3], c[4], c[5]), v0, e1, e2, t, u, v);
+        float* q = out + 4 * (size_t)i;
+        q[0] = h ? 1.0f : 0.0f;
+        q[1] = t;
+        q[2] = u;
+        q[3] = v;
+    } else if (op == 2) {
+        const float* c = in + 16 * (size_t)i;
+        DevLight L;
+        L.type = (int)c[0];
+        for (int k = 0; k < 3; ++k) {
+            L.color[k] = c[1 + k];
+            L.pos[k] = c[5 + k];
+            L.dir[k] = c[8 + k];
+        }
+        L.intensity = c[4];
+        L.cos_outer = c[11];
+        L.inv_cos_cone_diff = c[12];
+        V3 dir, rad;
+        light_sample(&L, 0, v3(c[13], c[14], c[15]), dir, rad);
+        float* q = out + 6 * (size_t)i;
+        q[0] = dir.x;
+        q[1] = dir.y;
+        q[2] = dir.z;
+        q[3] = rad.x;
+        q[4] = rad.y;
+        q[5] = rad.z;
+    } else if (op == 3) {
+        const float* c = in + 3 * (size_t)i;
+        for (int k = 0; k < 3; ++k) out[3 * (size_t)i + k] = (float)to_uchar(c[k]);
+    }
+}
+
+hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hot_kat, dim3((n + 255) / 256), dim3(256), 0, s, op, n, in, out);
+    return hipGetLastError();
 }
 
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false>
@@ -1222,11 +1319,11 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int32_t* hit, float* t,
-                             float* uv, hipStream_t s) {
+hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int mode, int32_t* hit,
+                             float* t, float* uv, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const size_t lds = (size_t)(a.stack_depth + 1) * 256 * sizeof(int);
-    hipLaunchKernelGGL(k_trace_rays, dim3((n + 255) / 256), dim3(256), lds, s, a, n, o, d, hit, t, uv);
+    const size_t lds = (size_t)kRaysLdsSlots * 256 * sizeof(int);
+    hipLaunchKernelGGL(k_trace_rays, dim3((n + 255) / 256), dim3(256), lds, s, a, n, o, d, mode, hit, t, uv);
     return hipGetLastError();
 }
 
