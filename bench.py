@@ -17,6 +17,16 @@ across the N GPUs, one gather to rank 0 (bounded by the heaviest pixels'
 serial sample chains).  value = rays of all frames /
 max-over-ranks step time.
 
+A step is the reference's doTrace (path_tracer.cu:491-554) in full: the
+world transform and BVH build (:536-542, transform + LBVH + the 4-wide
+traversal tree), setupRandSeed, the trace launches and copyToFB.
+
+Roofline: the trace kernel's working set is L1/L2
+resident, so its algorithmic bytes are set against the guide's L2-resident
+gather rate, and the binding resource is read from the rocprofv3 PMC summary
+of the same workload committed under profiles/ (VALU issue, lane
+utilisation, HBM bytes).
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -33,6 +43,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+# MI355X_MICROARCH.md "Indexed rows: gather into LDS": rows shared by every
+# workgroup (the XCD's L2) gather at 16.8-18.8 TB/s chip-wide -- the
+# cache-level ceiling for bytes the kernel re-reads from L1/L2
+L2_GATHER_PEAK_GBS = 18800.0
+# VALU issue: a wave64 VALU instruction holds a SIMD-32 for 2 cycles, 4 SIMDs
+# per CU, 256 CUs (MI355X_MICROARCH.md, "SIMD" and the cycle constants)
+VALU_INST_PER_CU_CYCLE = 2.0
+N_CU = 256
 # algorithmic bytes: binary internal visit = links 8 + 2 child
 # AABBs 48; 4-wide visit = links 16 + 4 child AABBs 96; leaf = fid 4 + 3
 # indices 12 + 3 vertices 36; shading hit = 3 normals 36 + 3 indices 12 +
@@ -67,6 +85,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--spp-per-launch", type=int, default=0)
+    ap.add_argument("--pipe-sets", type=int, default=0,
+                    help="launch pipeline band sets (tpt_params.pipe_sets): 0 auto, 1 one launch per frame")
     ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
     ap.add_argument("--refill", type=int, default=0, help="0 = library default")
     ap.add_argument("--extra-streams", type=int, default=0,
@@ -74,9 +94,9 @@ def parse():
                          "group's communicator streams would), to check the launch pipeline's queue use")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port on rank 0 at N=1")
     ap.add_argument("--cpu-spp", type=int, default=16)
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_trace_latest.json"),
-                    help="per-launch HBM bytes measured by rocprofv3 --pmc (tools/profile.sh)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every usable host core")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles"),
+                    help="rocprofv3 PMC summaries (tools/profile.sh); the one whose bench_config matches is used")
     args = ap.parse_args()
     if args.config:
         # preset values, unless the flag was given explicitly on the command line
@@ -120,32 +140,86 @@ def data_note(args):
     return f"{src}, seed {args.seed}, {env}"
 
 
+def usable_cores():
+    """Host cores this process may use: the affinity mask, capped by a cgroup
+    CPU quota and by OMP_NUM_THREADS (set to the box's CPU share on the GPU
+    pool).  Returns (threads, facts)."""
+    aff = len(os.sched_getaffinity(0))
+    facts = {"nproc": os.cpu_count(), "affinity": aff}
+    n = aff
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            facts["cgroup_cpu_quota"] = round(int(q) / int(per), 2)
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        facts["OMP_NUM_THREADS"] = int(omp)
+        n = min(n, int(omp))
+    return n, facts
+
+
+BASELINE_CFLAGS = ["-O3", "-march=native", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC", "-shared",
+                   "-std=c11", "-D_GNU_SOURCE"]
+
+
+def baseline_library():
+    """The CPU baseline build of the oracle: the same C
+    restatement compiled -O3 -march=native for THIS host (the checker build,
+    oracle/liboracle.so, is -O2 and portable).  Compiled into the temp dir on
+    first use; falls back to the checker build if no compiler is present."""
+    import subprocess
+    import tempfile
+    src = os.path.join(ROOT, "oracle", "tpt_oracle.c")
+    out = os.path.join(tempfile.gettempdir(), f"tpt_oracle_native_{os.getuid()}.so")
+    try:
+        if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+            subprocess.run(["gcc"] + BASELINE_CFLAGS + ["-o", out + ".tmp", src, "-lm"], check=True,
+                           capture_output=True, timeout=120)
+            os.replace(out + ".tmp", out)
+        return out, "gcc " + " ".join(BASELINE_CFLAGS)
+    except (OSError, subprocess.SubprocessError):
+        return None, "oracle/liboracle.so (checker build, -O2)"
+
+
 def cpu_baseline(args):
-    """The oracle (CPU port of the reference kernels) on the host cores: the
-    bench workload at a bounded spp (Mrays/s does not depend on spp), plus
+    """The oracle (CPU port of the reference kernels, identical BVH and
+    semantics) on the host cores, BASELINE.md section 3: -O3 -march=native,
+    OpenMP dynamic over pixel rows, every usable core, libm trig (trig_mode 0);
+    the bench workload at a bounded spp (Mrays/s does not depend on spp), plus
     SURVEY 8(d) C1 (box 256x256, 16 spp, depth 4).  Trace phase only (RNG init
-    reported separately, like the reference's per-frame curand_init); best of
-    3 runs each."""
+    reported separately, like the reference's per-frame curand_init); best of 3."""
     from oracle import oracle as O
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads, facts = usable_cores()
+    if args.cpu_threads > 0:
+        threads = args.cpu_threads
+    path, flags = baseline_library()
+    O.use_library(path)
 
     def best_of(ps, w, h, spp, depth, n=3):
         best = None
         for _ in range(n):
-            _, _, c = O.render(ps, w, h, spp, depth, args.seed, trig_mode=1, threads=threads)
+            _, _, c = O.render(ps, w, h, spp, depth, args.seed, trig_mode=0, threads=threads)
             if best is None or c["trace_ms"] < best["trace_ms"]:
                 best = c
         return best
 
-    ps = O.load_scene(scene_file(args.scene))
-    c = best_of(ps, args.width, args.height, args.cpu_spp, args.depth)
+    try:
+        ps = O.load_scene(scene_file(args.scene))
+        c = best_of(ps, args.width, args.height, args.cpu_spp, args.depth)
+        c1 = best_of(O.load_scene(scene_file("box")), 256, 256, 16, 4)
+    finally:
+        O.use_library(None)
     mrays = c["traversals"] / (c["trace_ms"] * 1e3)
-    c1 = best_of(O.load_scene(scene_file("box")), 256, 256, 16, 4)
     c1_mrays = c1["traversals"] / (c1["trace_ms"] * 1e3)
     return {"value": round(mrays, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{args.scene}.gltf {args.width}x{args.height} x {args.cpu_spp} spp, depth {args.depth}, "
                       f"seed {args.seed}, best of 3: {c['traversals']} rays in {c['trace_ms'] / 1e3:.2f} s trace "
                       f"(+{c['init_ms'] / 1e3:.2f} s RNG init not counted)",
+            "build": flags, "trig": "libm float (trig_mode 0)", "host": facts,
             "c1": {"value": round(c1_mrays, 3), "unit": "Mrays/s",
                    "sample": f"box.gltf 256x256 x 16 spp, depth 4, seed {args.seed}, best of 3: "
                              f"{c1['traversals']} rays in {c1['trace_ms'] / 1e3:.3f} s trace"},
@@ -161,6 +235,64 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def pmc_summary(args, world, config):
+    """The committed rocprofv3 PMC summary of this exact workload (tools/profile.sh
+    writes bench_config into it), or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(args.pmc_dir, "*pmc_summary*.json"))):
+        try:
+            with open(path) as f:
+                pm = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if pm.get("bench_config") == config and pm.get("n_gpus") == world:
+            best = (path, pm)
+    return best
+
+
+def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_launch_ms):
+    """The trace kernel against the MI355X ceilings.
+    Live: algorithmic bytes per step / step time, against the L2-resident gather
+    rate.  From the PMC summary of the same workload: per-step VALU
+    wave-instructions against the VALU issue ceiling at the measured clock, lane
+    utilisation, HBM bytes against 8 TB/s.  `bound` names the largest fraction."""
+    alg = bytes_step / step_s / 1e9
+    limits = {"l2_gather": {"achieved": round(alg, 1), "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(alg / L2_GATHER_PEAK_GBS, 4), "what": "algorithmic bytes (SURVEY 8(d))"}}
+    traffic = None
+    found = pmc_summary(args, world, config)
+    source = None
+    if found:
+        source, pm = found
+        source = os.path.relpath(source, ROOT)
+        c = pm.get("counters_per_launch", {})
+        lps = pm.get("launches_per_step") or launches_per_step
+        if pm.get("hbm_bytes_per_launch") is not None:
+            traffic = pm["hbm_bytes_per_launch"]
+            hbm = traffic * lps / step_s / 1e9
+            limits["hbm"] = {"achieved": round(hbm, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(hbm / HBM_PEAK_GBS, 6), "what": "2*FETCH_SIZE + WRITE_SIZE"}
+        clk = pm.get("effective_clock_ghz")
+        if c.get("SQ_INSTS_VALU") and clk:
+            inst = c["SQ_INSTS_VALU"] * lps / step_s / 1e9
+            peak = VALU_INST_PER_CU_CYCLE * N_CU * clk
+            limits["valu_issue"] = {"achieved": round(inst, 1), "peak": round(peak, 1), "unit": "G wave-inst/s",
+                                    "frac": round(inst / peak, 4), "clock_ghz": clk,
+                                    "lane_utilization": pm.get("valu_lane_utilization")}
+        for k in ("sq_wait_any_frac", "sq_active_inst_any_frac", "l2_hit_rate", "l1_miss_to_l2_frac",
+                  "lds_bank_conflict_cycles_per_lds_inst", "ta_accesses_per_cu_cycle"):
+            if pm.get(k) is not None:
+                limits.setdefault("pmc", {})[k] = pm[k]
+    bound = max((v["frac"], k) for k, v in limits.items() if "frac" in v)[1]
+    top = limits[bound]
+    return {"bound": {"l2_gather": "l2", "hbm": "hbm", "valu_issue": "valu"}[bound],
+            "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"], "frac": top["frac"],
+            "traffic": traffic, "kernel": "k_trace",
+            "bytes_per_step": bytes_step, "launches_per_step": launches_per_step,
+            "avg_launch_ms": round(avg_launch_ms, 3), "limits": limits, "pmc_source": source}
 
 
 def main():
@@ -191,9 +323,6 @@ def main():
     torch.cuda.synchronize()
     scene = T.Scene(scene_file(args.scene))
     d_scene = scene.copySceneToDevice(dev)
-    t0 = time.perf_counter()
-    d_scene.build()
-    build_ms = (time.perf_counter() - t0) * 1e3
     W, H = args.width, args.height
     pt = T.PathTracer("", W, H, dev)
     if args.env == "none":
@@ -211,10 +340,16 @@ def main():
     radiances = [torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}") for _ in range(n_frames)]
     flags = args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0)
 
+    build_ms = []
+
     def step():
+        # doTrace rebuilds the world transform and the BVH every frame (path_tracer.cu:536-542)
+        tb = time.perf_counter()
+        d_scene.build()
+        build_ms.append((time.perf_counter() - tb) * 1e3)
         st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
                               radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
-                              refill=args.refill)
+                              refill=args.refill, pipe_sets=args.pipe_sets)
         if world == 1:
             return st, radiances[0]
         src = radiances if args.dist_backend == "nccl" else [r.cpu() for r in radiances]   # gloo: host tensors
@@ -240,7 +375,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     keys = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
-            "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms"]
+            "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms", "local_rays"]
     local_tot = {k: float(sum(s[k] for s in stats)) for k in keys}
     vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64,
                        device=f"cuda:{dev}" if args.dist_backend == "nccl" else "cpu")
@@ -278,22 +413,13 @@ def main():
         K = args.steps
         rays = tot["traversals"]
         value = rays / elapsed / 1e6
-        # roofline of the dominant kernel (k_trace), per launch, rank 0's device
+        step_s = elapsed / K
+        # algorithmic bytes of the dominant kernel (k_trace), rank 0's device, per step
         l_tot = local_tot
         nl = max(l_tot["trace_launches"], 1.0)
-        bytes_total = (B_INNER * l_tot["internal_visits"] + B_WIDE * l_tot["wide_visits"] + B_LEAF * l_tot["leaf_tests"] +
-                       B_HIT * l_tot["shade_hits"] + B_PIX * l_tot["pixels"])
-        bytes_per_launch = bytes_total / nl
-        # avg_launch_s: each launch's own duration (HIP events on its stream;
-        # what rocprofv3 reports per kernel dispatch).  The launch pipeline runs
-        # launches of different band sets concurrently (concurrency = summed
-        # launch time / trace-phase wall time), so the kernel's byte rate is
-        # bytes per launch / (launch duration / concurrency) -- the algorithmic
-        # bytes of the trace phase over its wall time
-        avg_launch_s = (l_tot["trace_kernel_ms"] / nl) / 1e3
-        concurrency = l_tot["trace_kernel_ms"] / max(l_tot["trace_ms"], 1e-9)
-        achieved = bytes_per_launch * concurrency / avg_launch_s / 1e9
-        traffic = None
+        bytes_step = (B_INNER * l_tot["internal_visits"] + B_WIDE * l_tot["wide_visits"] + B_LEAF * l_tot["leaf_tests"]
+                      + B_HIT * l_tot["shade_hits"] + B_PIX * l_tot["pixels"]) / K
+        avg_launch_ms = l_tot["trace_kernel_ms"] / nl   # each launch's own HIP-event time (= rocprof's per dispatch)
         batch = (f" x {n_frames} frames (seeds {seeds[0]}..{seeds[-1]}), each banded across {ranks} ranks"
                  if n_frames > 1 else "")
         config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}"
@@ -301,28 +427,22 @@ def main():
                   "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
                   "max_depth": args.depth, "seed": args.seed,
                   "frames_per_step": n_frames,
+                  "step": "doTrace: transform + BVH build + setupRandSeed + trace + copyToFB (path_tracer.cu:491-554)",
+                  "launch_schedule": ("one launch per frame" if args.pipe_sets == 1 else
+                                      f"pipe_sets={args.pipe_sets}" if args.pipe_sets > 1 else "auto"),
                   "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + "
                                  + ("RCCL " if args.dist_backend == "nccl" else "gloo (1-GPU rehearsal) ")
                                  + ("all-to-all" if args.scaling == "weak" else "gather")
                   if world > 1 else ("1 GPU" if ranks == 1 else f"1 GPU, rank 0 of {ranks} emulated")}
-        if os.path.exists(args.pmc_json):
-            try:
-                with open(args.pmc_json) as f:
-                    pm = json.load(f)
-                # PMC bytes are per launch of the profiled workload: use them
-                # only when that was this exact single-GPU configuration
-                if pm.get("bench_config") == config and pm.get("n_gpus") == world:
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+        roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms)
         out = {
-            "metric": "Mrays/s at 1920x1080x1024spp (box.gltf, 8 bounces); achieved algorithmic GB/s vs HBM peak",
+            "metric": "Mrays/s at 1920x1080x1024spp (box.gltf, 8 bounces); achieved GB/s vs peak",
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / K * 1e3, 3),
+            "ms_per_step": round(step_s * 1e3, 3),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
@@ -331,19 +451,18 @@ def main():
             "config": config,
             "msamples_per_s": round(tot["samples"] / elapsed / 1e6, 2),
             "rays_per_sample": round(rays / max(tot["samples"], 1), 4),
+            # rays = reference-equivalent traverseBVH calls; of them, the direct probes
+            # resolved exactly in the shading pass without a BVH walk are local_rays
+            "gpu_traversals": int(tot["traversals"] - tot["local_rays"]),
+            "local_rays": int(tot["local_rays"]),
+            "bvh_traversals_per_s_M": round((tot["traversals"] - tot["local_rays"]) / elapsed / 1e6, 2),
             "visits_per_ray": {k: round(l_tot[k] / max(l_tot["traversals"], 1), 3)
                                for k in ("wide_visits", "internal_visits", "leaf_tests")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "kernel": "k_trace", "bytes_per_launch": bytes_per_launch,
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 3),
-                         "concurrency": round(concurrency, 3),
-                         "launches_per_step": nl / K},
-            "phases_ms_per_step": {"rng_init": round(l_tot["rng_init_ms"] / K, 3),
+            "roofline": roof,
+            "phases_ms_per_step": {"scene_build": round(sum(build_ms[-K:]) / K, 3),
+                                   "rng_init": round(l_tot["rng_init_ms"] / K, 3),
                                    "trace": round(l_tot["trace_ms"] / K, 3),
-                                   "resolve": round(l_tot["resolve_ms"] / K, 3),
-                                   "bvh_build_once": round(build_ms, 3)},
+                                   "resolve": round(l_tot["resolve_ms"] / K, 3)},
         }
         if world > 1 and args.verify_gather:
             # the assembled frame(s) must equal one GPU rendering every row (the

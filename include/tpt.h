@@ -130,6 +130,9 @@ typedef struct {
     uint64_t accumulated_spp;     /* samples per pixel in the output (> spp with TPT_FLAG_ACCUMULATE) */
     double trace_kernel_ms;       /* sum of the trace launches' own durations (HIP events per launch);
                                      > trace_ms when the launch pipeline overlaps them */
+    uint64_t local_rays;          /* of `traversals`, the direct probes resolved in the shading pass without
+                                     a BVH traversal (no emissive triangle, or a miss of the <= 4-emitter
+                                     inline test); traversals - local_rays = BVH traversals run */
 } tpt_stats;
 
 typedef struct tpt_scene tpt_scene;

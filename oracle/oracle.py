@@ -115,6 +115,20 @@ def lib():
     return _lib
 
 
+def use_library(path):
+    """Load the oracle from another build of tpt_oracle.c (bench.py's CPU
+    baseline: -O3 -march=native for the host), or back to liboracle.so (None)."""
+    global _lib
+    _lib = None
+    if path:
+        saved = globals()["LIB_PATH"]
+        globals()["LIB_PATH"] = path
+        try:
+            lib()
+        finally:
+            globals()["LIB_PATH"] = saved
+
+
 def _ptr(a, ct):
     return a.ctypes.data_as(C.POINTER(ct))
 

@@ -168,6 +168,12 @@ def test_render_parity(built, name, W, H, spp, depth, env, order):
     assert (fb[..., 3] == 0).all()
     # ray counts are deterministic; equal unless a diverged path took a different branch
     assert abs(stats["traversals"] - oc["traversals"]) <= 0.01 * oc["traversals"]
+    # probes resolved in the shading pass (no emitter / inline emitter test) are a subset
+    assert 0 <= stats["local_rays"] <= stats["traversals"]
+    if order == "reference":
+        assert stats["local_rays"] == 0
+    elif name in ("box", "box1", "light", "square"):   # box: inline emitter test; the others: no emitter
+        assert stats["local_rays"] > 0
     if m["bit_same"] == 1.0:
         assert stats["traversals"] == oc["traversals"]
         assert stats["shade_hits"] == oc["shade_hits"]

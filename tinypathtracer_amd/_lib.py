@@ -63,7 +63,8 @@ class Stats(C.Structure):
                 ("shade_hits", C.c_uint64), ("pixels", C.c_uint64), ("samples", C.c_uint64),
                 ("rng_init_ms", C.c_double), ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("total_ms", C.c_double), ("trace_launches", C.c_int32), ("pad", C.c_int32),
-                ("wide_visits", C.c_uint64), ("accumulated_spp", C.c_uint64), ("trace_kernel_ms", C.c_double)]
+                ("wide_visits", C.c_uint64), ("accumulated_spp", C.c_uint64), ("trace_kernel_ms", C.c_double),
+                ("local_rays", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}

@@ -866,6 +866,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         stats->traversals = cnt[0];
         stats->internal_visits = cnt[1];
         stats->wide_visits = cnt[5];
+        stats->local_rays = cnt[9];
         stats->accumulated_spp = total_spp;
         stats->leaf_tests = cnt[2];
         stats->shade_hits = cnt[3];

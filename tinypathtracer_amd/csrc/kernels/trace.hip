@@ -622,6 +622,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
     const bool active = x < a.width && ly < a.band_height && y < a.height;
     uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
+    uint32_t c_local = 0;   // rays resolved in the shading pass without a BVH traversal
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
     // frame batch: each frame owns its own RNG and accumulator planes
@@ -815,6 +816,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             // root with no hit, exactly as a traversal would (the ray
                             // is still counted: the reference traces it)
                             ++c_trav;
+                            ++c_local;
                             rec.put_dst(depth, mk, kNoProbe, direct);
                             after = true;
                         } else if (INL) {
@@ -828,6 +830,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                                 ++c_wide;
                                 emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf);
                                 if (r.fid < 0) {
+                                    ++c_local;
                                     rec.put_dst(depth, mk, kNoProbe, direct);
                                     after = true;
                                     begun = false;
@@ -998,7 +1001,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         g_acc[npix + off] = total.y;
         g_acc[2 * npix + off] = total.z;
     }
-    const unsigned long long s_wide = wave_sum(c_wide);
+    const unsigned long long s_wide = wave_sum(c_wide), s_local = wave_sum(c_local);
     const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
                              s_shade = wave_sum(c_shade), s_ovf = wave_sum(c_ovf);
 #ifdef TPT_PROFILE_PHASES
@@ -1025,6 +1028,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[3], s_shade);
         if (s_ovf) atomicAdd(&a.counters[4], s_ovf);
         atomicAdd(&a.counters[5], s_wide);
+        atomicAdd(&a.counters[9], s_local);
 #ifdef TPT_PROFILE_PHASES
         atomicAdd(&a.counters[6], p_done);
         atomicAdd(&a.counters[7], p_trav);

@@ -1,14 +1,17 @@
-# Full GPU evidence pass: parity suite, smoke, rocprof (kernel trace + PMC) of the
-# bench workload, then the bench itself (its roofline.traffic reads the PMC summary).
+#!/bin/bash
+# GPU evidence for one bench configuration: rocprofv3 kernel stats + PMC passes of
+# the workload (tools/profile.sh), the summary and the kernel-stats CSV copied
+# into profiles/, then the bench itself (its roofline reads that summary).
+# Usage: bash tools/gpu_round.sh TAG NAME [bench args]
+#   e.g. bash tools/gpu_round.sh r02 c2            (the default bench line)
+#        bash tools/gpu_round.sh r02 c3 --config C3
 set -o pipefail
 export TMPDIR=/tmp
-TAG=${1:-r01}
-mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1; echo PYTEST=$?
-tail -3 gpurun_out/pytest_gpu_$TAG.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { echo SMOKE FAILED; tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
-echo SMOKE=0; tail -1 gpurun_out/smoke_$TAG.log
-bash tools/profile.sh $TAG --steps 1 --warmup 0 --cpu-baseline 0 > gpurun_out/profile_$TAG.log 2>&1 || { echo PROFILE FAILED; tail -5 gpurun_out/profile_$TAG.log; exit 1; }
-echo PROF=0; grep -E "avg_duration|valu_lane|wait_any_frac|l2_hit|hbm_bytes|effective" gpurun_out/profile_$TAG.log
-cp gpurun_out/prof_$TAG/summary.json profiles/pmc_trace_latest.json
-timeout -k 10 900 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; echo BENCH=$?; tail -1 gpurun_out/bench_$TAG.json
+TAG=${1:-r02}; NAME=${2:-c2}; shift 2
+ARGS="$@"
+mkdir -p gpurun_out profiles
+bash tools/profile.sh ${TAG}_$NAME --steps 1 --warmup 0 --cpu-baseline 0 $ARGS > gpurun_out/profile_${TAG}_$NAME.log 2>&1 || { echo PROFILE FAILED; tail -5 gpurun_out/profile_${TAG}_$NAME.log; exit 1; }
+cp gpurun_out/prof_${TAG}_$NAME/summary.json profiles/${TAG}_pmc_summary_$NAME.json
+f=$(ls gpurun_out/prof_${TAG}_$NAME/ktrace/*/*kernel_stats.csv gpurun_out/prof_${TAG}_$NAME/ktrace/*kernel_stats.csv 2>/dev/null | head -1)
+[ -n "$f" ] && cp "$f" profiles/${TAG}_kernel_stats_$NAME.csv
+python3 -c 'import json,sys; s=json.load(open(sys.argv[1])); print({k: s.get(k) for k in ("avg_duration_ms","serialized_avg_duration_ms","effective_clock_ghz","valu_issue_frac_serialized","valu_lane_utilization","sq_wait_any_frac","l2_hit_rate","hbm_bytes_per_launch","lds_bank_conflict_cycles_per_lds_inst","ta_accesses_per_cu_cycle","launches_per_step")})' profiles/${TAG}_pmc_summary_$NAME.json

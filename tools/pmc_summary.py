@@ -1,4 +1,18 @@
-"""Summarise rocprofv3 PMC passes for the k_trace dispatches (per launch)."""
+"""Summarise the rocprofv3 passes of tools/profile.sh for the k_trace dispatches.
+
+counters_per_launch: mean over dispatches of each counter (summed over the
+chip).  Derived (MI355X_MICROARCH.md: SQ_*_CYCLES / SQ_ACTIVE_INST_* count
+quad-cycles, GRBM_GUI_ACTIVE sums 8 XCDs, gfx950 FETCH_SIZE reads 1/2 of the
+bytes, FETCH/WRITE_SIZE in KiB):
+  avg_duration_ms              dispatch duration as the bench runs them (kernel-trace pass)
+  serialized_avg_duration_ms   the same dispatches timed alone (PMC passes serialise them)
+  effective_clock_ghz          GRBM_GUI_ACTIVE / 8 / serialised duration
+  valu_issue_frac_serialized   SQ_INSTS_VALU * 2 cycles / (4 SIMDs * 256 CUs * cycles)
+  valu_lane_utilization        SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)
+  ta_accesses_per_cu_cycle     TCP_TOTAL_CACHE_ACCESSES / (256 CUs * cycles)
+  lds_bank_conflict_cycles_per_lds_inst
+  hbm_bytes_per_launch         2 * FETCH_SIZE + WRITE_SIZE (bytes)
+"""
 import csv
 import glob
 import json
@@ -7,6 +21,19 @@ import sys
 
 out_dir = sys.argv[1]
 kernel_key = sys.argv[2] if len(sys.argv) > 2 else "k_trace"
+N_CU = 256
+
+
+def durations(pattern):
+    d = {}
+    for path in glob.glob(os.path.join(out_dir, pattern, "**", "*kernel_trace.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kernel_key in row.get("Kernel_Name", ""):
+                    d[(path, row.get("Dispatch_Id"))] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
+    return list(d.values())
+
+
 vals = {}
 for path in glob.glob(os.path.join(out_dir, "pmc*", "**", "*counter_collection.csv"), recursive=True):
     with open(path) as f:
@@ -14,18 +41,22 @@ for path in glob.glob(os.path.join(out_dir, "pmc*", "**", "*counter_collection.c
             if kernel_key not in row.get("Kernel_Name", ""):
                 continue
             name = row["Counter_Name"]
-            vals.setdefault(name, {}).setdefault(row["Dispatch_Id"], 0.0)
-            vals[name][row["Dispatch_Id"]] += float(row["Counter_Value"])
+            key = (path, row["Dispatch_Id"])
+            vals.setdefault(name, {}).setdefault(key, 0.0)
+            vals[name][key] += float(row["Counter_Value"])
 per_launch = {k: sum(v.values()) / max(len(v), 1) for k, v in vals.items()}
-durs = []
-for path in glob.glob(os.path.join(out_dir, "ktrace", "**", "*kernel_trace.csv"), recursive=True):
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel_key in row.get("Kernel_Name", ""):
-                durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
+durs = durations("ktrace")
+sdurs = durations("pmc*")
 s = {"kernel": kernel_key, "launches_traced": len(durs),
-     "avg_duration_ms": sum(durs) / len(durs) if durs else None, "counters_per_launch": per_launch}
+     "avg_duration_ms": sum(durs) / len(durs) if durs else None,
+     "serialized_avg_duration_ms": sum(sdurs) / len(sdurs) if sdurs else None,
+     "counters_per_launch": per_launch}
 p = per_launch
+if p.get("GRBM_GUI_ACTIVE") and s["serialized_avg_duration_ms"]:
+    s["effective_clock_ghz"] = round(p["GRBM_GUI_ACTIVE"] / 8.0 / (s["serialized_avg_duration_ms"] * 1e6), 4)
+cycles = p["GRBM_GUI_ACTIVE"] / 8.0 if p.get("GRBM_GUI_ACTIVE") else None
+if cycles and p.get("SQ_INSTS_VALU"):
+    s["valu_issue_frac_serialized"] = p["SQ_INSTS_VALU"] * 2.0 / (4.0 * N_CU * cycles)
 if "SQ_THREAD_CYCLES_VALU" in p and p.get("SQ_ACTIVE_INST_VALU"):
     s["valu_lane_utilization"] = p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"])
 if p.get("SQ_WAVE_CYCLES"):
@@ -36,8 +67,11 @@ if "TCC_HIT_sum" in p and (p["TCC_HIT_sum"] + p.get("TCC_MISS_sum", 0)) > 0:
     s["l2_hit_rate"] = p["TCC_HIT_sum"] / (p["TCC_HIT_sum"] + p["TCC_MISS_sum"])
 if p.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
     s["l1_miss_to_l2_frac"] = p.get("TCP_TCC_READ_REQ_sum", 0) / p["TCP_TOTAL_CACHE_ACCESSES_sum"]
+    if cycles:
+        s["ta_accesses_per_cu_cycle"] = p["TCP_TOTAL_CACHE_ACCESSES_sum"] / (N_CU * cycles)
+if p.get("SQ_INSTS_LDS") and "SQ_LDS_BANK_CONFLICT" in p:
+    s["lds_bank_conflict_cycles_per_lds_inst"] = p["SQ_LDS_BANK_CONFLICT"] / p["SQ_INSTS_LDS"]
 if "FETCH_SIZE" in p or "WRITE_SIZE" in p:
-    # MI355X_MICROARCH.md HBM section: FETCH_SIZE/WRITE_SIZE in KiB; gfx950 FETCH_SIZE reads 1/2 of the bytes
     fetch = p.get("FETCH_SIZE", 0.0) * 1024.0
     write = p.get("WRITE_SIZE", 0.0) * 1024.0
     s["fetch_bytes_raw"] = fetch
@@ -53,11 +87,8 @@ try:
                 s["bench_config"] = b.get("config")
                 s["n_gpus"] = b.get("n_gpus")
                 s["bench_value"] = b.get("value")
+                s["bench_ms_per_step"] = b.get("ms_per_step")
                 s["launches_per_step"] = b.get("roofline", {}).get("launches_per_step")
 except OSError:
     pass
-# (launches that overlap each other -- the launch pipeline -- make the traced
-# durations longer than the GPU-busy time of one dispatch: no clock estimate)
-if p.get("GRBM_GUI_ACTIVE") and s.get("avg_duration_ms") and (s.get("launches_per_step") or 1) <= 1:
-    s["effective_clock_ghz"] = p["GRBM_GUI_ACTIVE"] / 8.0 / (s["avg_duration_ms"] * 1e6)
 print(json.dumps(s, indent=1))
