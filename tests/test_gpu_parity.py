@@ -172,7 +172,7 @@ def test_render_parity(built, name, W, H, spp, depth, env, order):
     assert 0 <= stats["local_rays"] <= stats["traversals"]
     if order == "reference":
         assert stats["local_rays"] == 0
-    elif name in ("box", "box1", "light", "square"):   # box: inline emitter test; the others: no emitter
+    elif name in ("box", "box1", "square"):   # box: inline emitter test; box1, square: no emitter
         assert stats["local_rays"] > 0
     if m["bit_same"] == 1.0:
         assert stats["traversals"] == oc["traversals"]

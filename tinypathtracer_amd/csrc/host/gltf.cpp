@@ -257,14 +257,21 @@ static const uint8_t* accessor_ptr(const json::Value& model, const std::vector<s
     const json::Value& v = (*views)[(size_t)bv];
     long long b = v.int_or("buffer", 0);
     if (b < 0 || (size_t)b >= bufs.size()) throw parse_error("bad buffer index");
-    long long off = a.int_or("byteOffset", 0) + v.int_or("byteOffset", 0);
+    const long long aoff = a.int_or("byteOffset", 0), voff = v.int_or("byteOffset", 0);
     *count = a.int_or("count", 0);
     *ctype = a.int_or("componentType", 0);
     std::string type = a.string_or("type", "SCALAR");
     *ncomp = type == "VEC2" ? 2 : type == "VEC3" ? 3 : type == "VEC4" ? 4 : 1;
     size_t csize = (*ctype == 5120 || *ctype == 5121) ? 1 : (*ctype == 5122 || *ctype == 5123) ? 2 : 4;
-    size_t need = (size_t)off + (size_t)(*count) * (size_t)(*ncomp) * csize;
-    if (need > bufs[(size_t)b].size()) throw parse_error("accessor exceeds buffer");
+    // untrusted offsets and counts: non-negative, and off + count * ncomp * csize
+    // within the buffer without overflowing
+    const size_t size = bufs[(size_t)b].size();
+    if (aoff < 0 || voff < 0 || *count < 0) throw parse_error("negative accessor offset or count");
+    if ((unsigned long long)aoff > size || (unsigned long long)voff > size - (size_t)aoff)
+        throw parse_error("accessor exceeds buffer");
+    const size_t off = (size_t)aoff + (size_t)voff;
+    const size_t elem = (size_t)(*ncomp) * csize;
+    if ((unsigned long long)*count > (size - off) / elem) throw parse_error("accessor exceeds buffer");
     return bufs[(size_t)b].data() + off;
 }
 
@@ -275,7 +282,7 @@ static std::vector<float> read_vec3(const json::Value& model, const std::vector<
     const uint8_t* p = accessor_ptr(model, bufs, acc, &count, &ctype, &ncomp);
     if (ctype != 5126 || ncomp != 3) throw parse_error("expected float VEC3 accessor");
     std::vector<float> out((size_t)count * 3);
-    std::memcpy(out.data(), p, out.size() * 4);
+    if (!out.empty()) std::memcpy(out.data(), p, out.size() * 4);
     return out;
 }
 

@@ -53,6 +53,9 @@ struct Huffman {
             valoff[len] = k - code;
             if (counts[len - 1]) {
                 for (int i = 0; i < counts[len - 1]; ++i, ++k, ++code) {
+                    // a code must fit in len bits (libjpeg: JERR_BAD_HUFF_TABLE); checked
+                    // before it indexes the lookahead table
+                    if (code >= (1 << len)) throw DecodeError("bad Huffman table");
                     if (len <= 9) {
                         const int shift = 9 - len;
                         for (int f = 0; f < (1 << shift); ++f)

@@ -35,9 +35,14 @@ struct Value {
         const Value* v = find(key);
         return (v && v->kind == Number) ? v->num : dflt;
     }
-    long long int_or(const std::string& key, long long dflt) const {
+    // Integer field; a number outside +-2^62 (or NaN) is out of range for any
+    // index, offset or count and reads as `bad` (the double -> integer cast
+    // would be undefined behaviour there).
+    long long int_or(const std::string& key, long long dflt, long long bad = -1) const {
         const Value* v = find(key);
-        return (v && v->kind == Number) ? (long long)v->num : dflt;
+        if (!v || v->kind != Number) return dflt;
+        if (!(v->num >= -4.6e18 && v->num <= 4.6e18)) return bad;
+        return (long long)v->num;
     }
     std::string string_or(const std::string& key, const std::string& dflt) const {
         const Value* v = find(key);
@@ -63,6 +68,15 @@ public:
 private:
     const std::string& s_;
     size_t i_;
+    int depth_ = 0;   // open containers; glTF nests a few levels, a hostile file thousands
+    static constexpr int kMaxDepth = 128;
+    struct Nest {
+        Parser& p;
+        explicit Nest(Parser& q) : p(q) {
+            if (++p.depth_ > kMaxDepth) p.fail("nesting too deep");
+        }
+        ~Nest() { --p.depth_; }
+    };
 
     [[noreturn]] void fail(const char* what) {
         throw std::runtime_error(std::string("json: ") + what + " at offset " + std::to_string(i_));
@@ -82,6 +96,7 @@ private:
         char c = s_[i_];
         Value v;
         if (c == '{') {
+            Nest nest(*this);
             v.kind = Value::Object;
             ++i_;
             ws();
@@ -100,6 +115,7 @@ private:
                 fail("expected ',' or '}'");
             }
         } else if (c == '[') {
+            Nest nest(*this);
             v.kind = Value::Array;
             ++i_;
             ws();

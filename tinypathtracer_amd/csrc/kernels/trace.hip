@@ -1151,6 +1151,10 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
                 trav_lane<true>(r, a, stk, c_ovf);
             }
             fid = (mode == 3 && r.mode == TM_OCCLUDED) ? -2 : r.fid;
+            if (mode == 3 && fid >= 0) {   // a closest-hit probe (no emissive tree) may end on a non-emitter
+                const int m = __float_as_int(a.shade[3 * fid].w);
+                if (a.mtl[2 * m].w == 0.0f) fid = -2;
+            }
         }
         hit[i] = fid;
         t[i] = r.t;
