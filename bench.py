@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--spp-per-launch", type=int, default=0)
+    ap.add_argument("--lanes-per-pixel", type=int, default=0,
+                    help="tpt_params.lanes_per_pixel: 0 auto, 1, 2 = pair mode (delta-light scenes)")
     ap.add_argument("--pipe-sets", type=int, default=0,
                     help="launch pipeline band sets (tpt_params.pipe_sets): 0 auto, 1 one launch per frame")
     ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
@@ -349,7 +351,8 @@ def main():
         build_ms.append((time.perf_counter() - tb) * 1e3)
         st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
                               radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
-                              refill=args.refill, pipe_sets=args.pipe_sets)
+                              refill=args.refill, pipe_sets=args.pipe_sets,
+                              lanes_per_pixel=args.lanes_per_pixel)
         if world == 1:
             return st, radiances[0]
         src = radiances if args.dist_backend == "nccl" else [r.cpu() for r in radiances]   # gloo: host tensors
@@ -430,6 +433,7 @@ def main():
                   "step": "doTrace: transform + BVH build + setupRandSeed + trace + copyToFB (path_tracer.cu:491-554)",
                   "launch_schedule": ("one launch per frame" if args.pipe_sets == 1 else
                                       f"pipe_sets={args.pipe_sets}" if args.pipe_sets > 1 else "auto"),
+                  "lanes_per_pixel": args.lanes_per_pixel or "auto",
                   "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + "
                                  + ("RCCL " if args.dist_backend == "nccl" else "gloo (1-GPU rehearsal) ")
                                  + ("all-to-all" if args.scaling == "weak" else "gather")

@@ -102,6 +102,11 @@ typedef struct {
      * one after the other (-25 % measured).  A host application that issues its own
      * greatest-priority work on the device while tpt_render runs shares those queues. */
     int32_t pipe_sets, pipe_chunks;
+    /* Lanes per pixel: 0 = auto, 1, or 2 = pair mode (scenes with delta lights): a side
+     * lane per pixel traces each bounce's shadow rays while the path lane goes on, so a
+     * sample's serial chain pays one traversal per bounce.
+     * Bit-identical either way. */
+    int32_t lanes_per_pixel;
 } tpt_params;
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */

@@ -226,6 +226,56 @@ def test_render_parity_full_resolution(built, name, W, H, spp, depth, env):
             assert st["trace_launches"] > 3
 
 
+@pytest.mark.parametrize("name,W,H,spp,depth,env", [("ball", 64, 36, 16, 8, "sky"), ("square", 64, 36, 16, 8, None),
+                                                    ("ball", 48, 30, 6, 32, "sky"), ("square", 40, 24, 8, 1, None)])
+def test_pair_mode_parity(built, name, W, H, spp, depth, env):
+    """Pair mode (lanes_per_pixel=2: a side lane per pixel traces the shadow
+    rays): bit-identical to one lane per pixel and to the oracle, ray counts
+    unchanged; banded and launch-pipelined schedules too."""
+    s, d, o = built[name]
+    sky = T.procedural_sky(64, 32) if env else None
+    pt = T.PathTracer("", W, H, 0)
+    if env:
+        pt.envLight = T.EnvLight(sky, 0)
+    one = np.zeros((H, W, 3), np.float32)
+    fb1 = np.zeros((H, W, 4), np.uint8)
+    st1 = pt.doTrace(d, s.m_camera, fb1, spp, seed=42, max_depth=depth, radiance=one, lanes_per_pixel=1)
+    two = np.zeros((H, W, 3), np.float32)
+    fb2 = np.zeros((H, W, 4), np.uint8)
+    st2 = pt.doTrace(d, s.m_camera, fb2, spp, seed=42, max_depth=depth, radiance=two, lanes_per_pixel=2)
+    assert np.array_equal(_bits(two), _bits(one))
+    assert np.array_equal(fb2, fb1)
+    assert st2["traversals"] == st1["traversals"] and st2["shade_hits"] == st1["shade_hits"]
+    orad, _, oc = O.render(o, W, H, spp, depth, 42, env=sky[::-1].copy() if env else None, trig_mode=1)
+    assert np.array_equal(_bits(two), _bits(orad))
+    assert st2["traversals"] == oc["traversals"]
+    banded = np.zeros((H, W, 3), np.float32)
+    for idx in range(3):
+        pt.doTrace(d, s.m_camera, None, spp, seed=42, max_depth=depth, radiance=banded, band=(8, 3, idx),
+                   lanes_per_pixel=2)
+    assert np.array_equal(_bits(banded), _bits(one))
+    piped = np.zeros((H, W, 3), np.float32)
+    pt.doTrace(d, s.m_camera, None, spp, seed=42, max_depth=depth, radiance=piped, lanes_per_pixel=2,
+               pipe_sets=2, pipe_chunks=3)
+    assert np.array_equal(_bits(piped), _bits(one))
+
+
+def test_pair_mode_full_resolution_c3(built):
+    """C3 (ball + sky) at 1920x1080, 2 spp, in pair mode: bit-exact vs the oracle."""
+    s, d, o = built["ball"]
+    W, H, spp = 1920, 1080, 2
+    sky = T.procedural_sky(2048, 1024)
+    orad, obgra, oc = O.render(o, W, H, spp, 8, 42, env=sky[::-1].copy(), trig_mode=1)
+    pt = T.PathTracer("", W, H, 0)
+    pt.envLight = T.EnvLight(sky, 0)
+    fb = np.zeros((H, W, 4), np.uint8)
+    rad = np.zeros((H, W, 3), np.float32)
+    st = pt.doTrace(d, s.m_camera, fb, spp, seed=42, radiance=rad, lanes_per_pixel=2)
+    assert np.array_equal(_bits(rad), _bits(orad))
+    assert np.array_equal(fb[..., :3], obgra[..., :3])
+    assert st["traversals"] == oc["traversals"]
+
+
 @pytest.mark.parametrize("name", ["ball", "box1", "box"])
 def test_env_importance_sampling_parity(built, name):
     """TPT_FLAG_ENV_IS (A15 re-derived, opt-in): env next-event estimation at

@@ -82,6 +82,7 @@ struct TraceArgs {
     int32_t any_emitter;                 // some triangle emits (else a direct probe adds nothing)
     int32_t emit_root;                   // inner4 id of the emissive-triangle tree (-1: none)
     int32_t emit_inline;                 // that tree is one node of leaves: probe pass 1 in the shading pass
+    int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
     int32_t stack_lds_slots;             // set by launch_trace: stack slots held in LDS (rest private)

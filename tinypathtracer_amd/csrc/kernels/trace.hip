@@ -556,7 +556,10 @@ __device__ __noinline__ bool env_is_sample(const TraceArgs& a, V3 nf, uint32_t s
     k_le = k * le;
     return true;
 }
-enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2 };
+// TS_IDLE (pair mode): a side lane without a job, or a path lane waiting for
+// its side lane's direct sum before the unwind -- neither traverses nor shades
+enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2, TS_IDLE = 3 };
+enum : int { PH_WAIT = 5 };   // pair mode: path lane waiting to unwind
 
 // Per-lane path records (path_tracer.cu:315-318), consumed by the unwind
 // (:416-430).  The reference keeps attenuation = baseColor * atten (3 floats),
@@ -579,22 +582,28 @@ __device__ __forceinline__ uint32_t p_kind(float prob) {
     return pb == 0x80000000u ? 1u : (pb == 0u ? 2u : 0u);
 }
 
-template <int MAXD>
+// RS: LDS columns per workgroup (256: one per lane; 128 in pair mode, one per
+// pixel -- the side lanes keep no records).
+template <int MAXD, int RS = 256>
 struct PathRecords {
-    TPT_LDS float* lds;                        // this lane's column: word at lds[(level*words + w) * 256]
+    TPT_LDS float* lds;                        // this lane's column: word at lds[(level*words + w) * RS]
     int nlds, words;
     float deep[MAXD * 5];
 
     __device__ __forceinline__ void put(int level, int w, float v) {
-        if (level < nlds) lds[(level * words + w) * 256] = v;
+        if (level < nlds) lds[(level * words + w) * RS] = v;
         else deep[level * 5 + w] = v;
     }
     __device__ __forceinline__ float get(int level, int w) const {
-        return level < nlds ? lds[(level * words + w) * 256] : deep[level * 5 + w];
+        return level < nlds ? lds[(level * words + w) * RS] : deep[level * 5 + w];
     }
-    // mk = material id | p-kind << 30; probe = material the probe hit (kNoProbe: none)
+    // mk = material id | p-kind << 30; probe = material the probe hit (kNoProbe: none).
+    // Pair mode (5 words, PACKED_PROBE): w1 = mk | probe << 15 as in the 2-word
+    // records and w2..w4 = the delta lights' direct sum alone, written by whichever
+    // lane traced the shadow rays; the unwind adds the probe's emission to it.
+    template <bool PACKED_PROBE = false>
     __device__ __forceinline__ void put_dst(int level, uint32_t mk, uint32_t probe, V3 dst) {
-        if (words == 2) {
+        if (words == 2 || PACKED_PROBE) {
             put(level, 1, __uint_as_float(mk | (probe << 15)));
         } else {
             put(level, 1, __uint_as_float(mk));
@@ -608,8 +617,24 @@ struct PathRecords {
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
 // state (direct term, normal, light index, incoming direction -- r.d during an
 // extension ray) is dead across traversals and drops out of the registers.
-template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false>
+//
+// PAIR (pair mode, delta-light scenes; DESIGN.md section 5 "Pair mode"): two
+// lanes per pixel, 8x4 pixels per wave.  The even lane runs the pixel's path
+// exactly as above; the odd lane is its side lane: when the path lane shades a
+// hit while its side lane is idle, it hands that bounce's shadow rays
+// (origin, material, level) to the side lane and goes straight on to the
+// probe and the next extension ray.  The side lane traces the level's shadow
+// rays in light order, sums the direct term exactly as the path lane would
+// and hands it back; the path lane stores it in that level's record and waits
+// for it, if need be, before the unwind.  Shadow rays consume no random
+// numbers, so every pixel's XORWOW stream is consumed as in the reference, and
+// each level's direct term is the same sum in the same order: the image is
+// bit-identical.  A pixel's sample chain then pays one traversal per bounce
+// instead of 1 + lights, which is what bounds tail-heavy frames (C3).
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
+          bool PAIR = false>
 __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
+    static_assert(!PAIR || (ORDERED && LIGHTS && !ENVIS), "pair mode: ordered delta-light variants");
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // grid y interleaves the frames of a batch: consecutive workgroups render the
@@ -617,10 +642,15 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     // screen locality of a single frame (node reuse in L1/L2)
     const int nfr = a.n_frames > 0 ? a.n_frames : 1;
     const int frame = (int)blockIdx.y % nfr;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = ((int)blockIdx.y / nfr) * 16 + (wave >> 1) * 8 + (lane >> 3);
+    // pair mode: lane 2q (path) and 2q + 1 (side) serve pixel q of the wave's 8x4 tile
+    const bool side = PAIR && (lane & 1);
+    const int pl = PAIR ? (lane >> 1) : lane;   // pixel slot in the wave
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (pl & 7);
+    const int ly = PAIR ? ((int)blockIdx.y / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3)
+                        : ((int)blockIdx.y / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
     const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
-    const bool active = x < a.width && ly < a.band_height && y < a.height;
+    const bool pixel = x < a.width && ly < a.band_height && y < a.height;
+    const bool active = pixel && !side;   // owns the pixel's RNG stream and sums
     uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
     uint32_t c_local = 0;   // rays resolved in the shading pass without a BVH traversal
     const size_t npix = (size_t)a.width * (size_t)a.height;
@@ -664,8 +694,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     LaneStack<StackT> stk;
     stk.lds = (TPT_LDS StackT*)(slds + a.lds_stack_offset) + ((TPT_STACK_PAIRED && sizeof(StackT) == 2) ? 2 * tid : tid);
     stk.nlds = a.stack_lds_slots;
-    PathRecords<MAXD> rec;
-    rec.lds = (TPT_LDS float*)(slds + a.lds_rec_offset) + tid;
+    PathRecords<MAXD, PAIR ? 128 : 256> rec;
+    rec.lds = (TPT_LDS float*)(slds + a.lds_rec_offset) + (PAIR ? wave * 32 + pl : tid);
     rec.nlds = a.rec_lds_levels;
     rec.words = LIGHTS ? 5 : 2;
 
@@ -685,8 +715,31 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     V3 rd = v3(0.0f, 0.0f, 0.0f), nd = rd, nrm = rd, direct = rd;
     Trav r;
     trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), TM_CLOSEST);
-    int ts = active ? TS_DONE : TS_DEAD;
+    int ts = active ? TS_DONE : ((PAIR && side && pixel) ? TS_IDLE : TS_DEAD);
     const int refill = a.refill;
+    // pair mode state.  Path lane: partner idle?, the level whose shadow rays the
+    // partner holds (-1: none), this level's shadows delegated?, the unwind's seed
+    // while waiting for the partner, a job to post at the next exchange.  Side
+    // lane: the level it works on and the direct sum it hands back.
+    bool p_idle = true, delegated = false, post = false, ready = false;
+    int pend = -1, jlevel = 0;
+    V3 Lwait = v3(0.0f, 0.0f, 0.0f);
+    // a level's record: pm = the material the probe hit (kNoProbe: none), dl =
+    // its direct term (delta lights + probe emission).  Pair mode keeps the
+    // probe symbolic and the delta lights' sum apart (the side lane may still be
+    // summing it); the unwind adds them in the same order, (1 * e) + direct.
+    auto put_level = [&](uint32_t pm, V3 dl) {
+        if constexpr (PAIR) {
+            rec.template put_dst<true>(depth, mk, pm, dl);
+            if (!delegated) {
+                rec.put(depth, 2, direct.x);
+                rec.put(depth, 3, direct.y);
+                rec.put(depth, 4, direct.z);
+            }
+        } else {
+            rec.put_dst(depth, mk, pm, dl);
+        }
+    };
 
 #ifdef TPT_PROFILE_PHASES
     const unsigned long long t_wave0 = wall_clock64();
@@ -760,6 +813,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     mk = (uint32_t)mtl | (p_kind(prob) << 30);
                     direct = v3(0.0f, 0.0f, 0.0f);
                     li = 0;
+                    delegated = false;
                     env_pending = ENVIS && !(m1.x > 0.0f) && !(m1.y > 0.0f);   // diffuse hit
                     lights_next = true;
                 }
@@ -781,14 +835,33 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 if (r.fid >= 0 && r.mode != TM_OCCLUDED) {   // the closest hit (an unbeaten emitter, pass 2)
                     pm = (uint32_t)__float_as_int(a.shade[3 * r.fid].w);
                     const float e = MT(2 * pm).w;
-                    dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + dl;
+                    if (!PAIR) dl = (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + dl;   // pair mode: at the unwind
                 }
-                rec.put_dst(depth, mk, pm, dl);
+                put_level(pm, dl);
                 after = true;
+            } else if (PAIR && phase == PH_WAIT) {   // the side lane's direct sum has arrived
+                L = Lwait;
+                finish = true;
             }
             TPT_SEC(1)
             V3 td = rd;
             bool shadow = false;
+            if (PAIR && lights_next && !side && li == 0 && p_idle) {
+                // hand this bounce's shadow rays to the idle side lane (posted at the
+                // exchange below: origin r.o, material mk, level depth)
+                post = true;
+                jlevel = depth;
+                pend = depth;
+                p_idle = false;
+                delegated = true;
+                li = a.n_lights;
+            }
+            if (PAIR && lights_next && side && li >= a.n_lights) {
+                // the side lane's job is done: its direct sum goes back at the exchange
+                ready = true;
+                ts = TS_IDLE;
+                lights_next = false;
+            }
             if (lights_next) {
                 const float4 m1 = MT(2 * (mk & 0x3fffffffu) + 1);
                 if (LIGHTS && li < a.n_lights) {
@@ -817,7 +890,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             // is still counted: the reference traces it)
                             ++c_trav;
                             ++c_local;
-                            rec.put_dst(depth, mk, kNoProbe, direct);
+                            put_level(kNoProbe, direct);
                             after = true;
                         } else if (INL) {
                             // <= 4 emitters: pass 1 here; a miss resolves the probe in
@@ -831,7 +904,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                                 emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf);
                                 if (r.fid < 0) {
                                     ++c_local;
-                                    rec.put_dst(depth, mk, kNoProbe, direct);
+                                    put_level(kNoProbe, direct);
                                     after = true;
                                     begun = false;
                                 } else {
@@ -843,7 +916,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             phase = PH_PROBE;
                         }
                     } else {
-                        rec.put_dst(depth, mk, kNoProbe, direct);
+                        put_level(kNoProbe, direct);
                         after = true;
                     }
                 }
@@ -863,12 +936,19 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 }
             }
             TPT_SEC(3)
+            if (PAIR && finish && pend >= 0) {
+                // the side lane still sums a level's shadow rays: wait for it (exchange below)
+                Lwait = L;
+                phase = PH_WAIT;
+                ts = TS_IDLE;
+                finish = false;
+            }
             if (finish) {   // unwind (:416-431): levels depth-1 .. 0
                 for (int k = depth - 1; k >= 0; --k) {
                     const float af = rec.get(k, 0);
                     const uint32_t w1 = __float_as_uint(rec.get(k, 1));
                     const bool packed = rec.words == 2;
-                    const float4 mb = MT(2 * (w1 & (packed ? 0x7fffu : 0x3fffffffu)));
+                    const float4 mb = MT(2 * (w1 & ((packed || PAIR) ? 0x7fffu : 0x3fffffffu)));
                     const V3 att = af * v3(mb.x, mb.y, mb.z);                   // :379
                     const uint32_t kind = w1 >> 30;
                     const float prob = kind == 0u ? af : (kind == 1u ? -0.0f : 0.0f);
@@ -879,6 +959,11 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                         const float e = pm == kNoProbe ? 0.0f : MT(2 * pm).w;
                         dst = pm == kNoProbe ? v3(0.0f, 0.0f, 0.0f)
                                              : (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + v3(0.0f, 0.0f, 0.0f);
+                    } else if (PAIR) {   // the delta lights' sum, then the probe's emission (1 * e) + direct
+                        const uint32_t pm = (w1 >> 15) & 0x7fffu;
+                        const V3 dd = v3(rec.get(k, 2), rec.get(k, 3), rec.get(k, 4));
+                        const float e = pm == kNoProbe ? 0.0f : MT(2 * pm).w;
+                        dst = pm == kNoProbe ? dd : (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + dd;
                     } else {
                         dst = v3(rec.get(k, 2), rec.get(k, 3), rec.get(k, 4));
                     }
@@ -914,7 +999,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 }
             }
             TPT_SEC(5)
-            if (ts != TS_DEAD) {
+            if (ts != TS_DEAD && ts != TS_IDLE) {
                 if (!begun) {
                     ++c_trav;
                     trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
@@ -923,6 +1008,45 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 ts = TS_TRAV;
             }
             TPT_SEC(6)
+        }
+        if constexpr (PAIR) {
+            // ---- exchange between a pixel's path lane and its side lane (whole wave) ----
+            // path -> side: a bounce's shadow rays (the path lane's r.o is that hit
+            // point until its next hit: a posting pass only starts rays from it)
+            const int jpost = __shfl_xor((int)post, 1, 64);
+            const float jx = __shfl_xor(r.o.x, 1, 64), jy = __shfl_xor(r.o.y, 1, 64), jz = __shfl_xor(r.o.z, 1, 64);
+            const int jmk = __shfl_xor((int)mk, 1, 64), jl = __shfl_xor(jlevel, 1, 64);
+            if (side && jpost) {
+                mk = (uint32_t)jmk;
+                jlevel = jl;
+                li = 0;
+                direct = v3(0.0f, 0.0f, 0.0f);
+                V3 ldir, lrad;
+                const V3 jo = v3(jx, jy, jz);
+                light_sample(a.lights, 0, jo, ldir, lrad);
+                ++c_trav;
+                trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root);
+                phase = PH_SHADOW;
+                ts = TS_TRAV;
+            }
+            post = false;
+            // side -> path: the level's direct sum, in light order
+            const int jready = __shfl_xor((int)ready, 1, 64);
+            const float dx = __shfl_xor(direct.x, 1, 64), dy = __shfl_xor(direct.y, 1, 64),
+                        dz = __shfl_xor(direct.z, 1, 64);
+            const int rl = __shfl_xor(jlevel, 1, 64);
+            if (!side && jready) {
+                rec.put(rl, 2, dx);
+                rec.put(rl, 3, dy);
+                rec.put(rl, 4, dz);
+                pend = -1;
+                p_idle = true;
+                if (phase == PH_WAIT) ts = TS_DONE;
+            }
+            ready = false;
+            // a path lane with no samples left retires its side lane
+            const int pdead = __shfl_xor((int)(ts == TS_DEAD), 1, 64);
+            if (side && ts == TS_IDLE && pdead) ts = TS_DEAD;
         }
         if (__ballot(ts != TS_DEAD) == 0ull) break;
 #ifdef TPT_PROFILE_PHASES
@@ -1226,21 +1350,23 @@ hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipSt
     return hipGetLastError();
 }
 
-template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false>
+template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
+          bool PAIR = false>
 static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR>), grid, dim3(256), lds, s, a);
 }
 
 // INL: probe pass 1 in the shading pass (an emissive tree of one node); its own
-// variant, so scenes with larger emitter sets keep the leaner kernel
-template <bool LIGHTS, bool MTL_LDS, typename StackT>
+// variant, so scenes with larger emitter sets keep the leaner kernel.  PAIR:
+// pair mode (delta-light scenes only).
+template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false>
 static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     if (a.emit_inline) {
-        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, false, true>(a, grid, lds, s);
-        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, false, true>(a, grid, lds, s);
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, false, true, PAIR>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, false, true, PAIR>(a, grid, lds, s);
     } else {
-        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
-        else launch_one<64, true, LIGHTS, MTL_LDS, StackT>(a, grid, lds, s);
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, false, false, PAIR>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, false, false, PAIR>(a, grid, lds, s);
     }
 }
 
@@ -1250,7 +1376,7 @@ constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
 constexpr size_t kLdsMtlMax = 2048;    // material tables up to 64 entries go to LDS
 constexpr size_t kLdsNodesMax = TPT_LDS_NODES_MAX;
 
-size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide) {
+size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide, int rec_cols = 256) {
     // [material table][top 4-wide nodes][traversal stack][path records].
     // Priorities (measured on box): the whole stack (a
     // stack capped at 23 of its 40 slots cost 7 %), then path records up to
@@ -1261,7 +1387,7 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
     a.lds_mtl_offset = 0;
     const size_t budget = kLdsBudget - mtl_bytes;
     const size_t slot = 256 * elem;
-    const size_t level = (size_t)words * 256 * sizeof(float);
+    const size_t level = (size_t)words * (size_t)rec_cols * sizeof(float);
     // whole stack (capacity + 3 spare slots for the unconditional 4-wide
     // pushes) when 2 record levels still fit; else its first slots, the rest private
     size_t slots = (size_t)a.stack_depth + 3;
@@ -1300,6 +1426,20 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
     const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
     const bool mtl_lds = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
+    // pair mode: delta lights (shadow rays to hand off), packed probe ids
+    const bool pair = a.pair && lights && a.n_lights > 0 && (a.n_materials + 1) < (int)kNoProbe;
+    if (pair) {
+        grid.y = ((a.band_height + 7) / 8) * (a.n_frames > 0 ? a.n_frames : 1);   // 16x8 pixels per workgroup
+        const size_t lds = trace_lds_bytes(a, 5, small ? 2 : 4, mtl_lds, true, 128);
+        if (mtl_lds) {
+            if (small) launch_ordered<true, true, uint16_t, true>(a, grid, lds, s);
+            else launch_ordered<true, true, int, true>(a, grid, lds, s);
+        } else {
+            if (small) launch_ordered<true, false, uint16_t, true>(a, grid, lds, s);
+            else launch_ordered<true, false, int, true>(a, grid, lds, s);
+        }
+        return hipGetLastError();
+    }
     const size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true);
     if (lights) {
         if (mtl_lds) {
