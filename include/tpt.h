@@ -114,6 +114,11 @@ typedef struct {
 #define TPT_FLAG_ENV_IS        0x8   /* opt-in env next-event estimation with importance sampling (A15
                                         re-derived; the reference's trace never calls it, so the image
                                         differs from a reference render) */
+#define TPT_FLAG_APPROX_CULL   0x10  /* the ordered traversal's culls without the exactness guards (no
+                                        position slack, no sliver re-test): a few
+                                        percent faster, and rays whose Moller-Trumbore t is rounding noise
+                                        (sliver triangles, grazing edge hits) may then find another hit
+                                        than the reference (5 of ~60 G rays over the BASELINE frames) */
 #define TPT_FLAG_ACCUMULATE    0x4   /* progressive: continue the previous call's per-pixel streams and
                                         sums (same frame size, bands and seed); the output is the mean over
                                         all accumulated samples, bit-identical to one call with their total */
@@ -178,7 +183,11 @@ void tpt_image_free(uint8_t* rgba);
  *                 host or device pointer (detected).  Only band rows written.
  *   bgra_out:     nullable, width*height*4 bytes, row 0 = top, B,G,R written,
  *                 alpha untouched (copyToFB, path_tracer.cu:451-471).
- *   env:          nullable -> black on miss. */
+ *   env:          nullable -> black on miss.
+ * Device outputs are written on the library's own stream and are complete when
+ * tpt_render returns; no other stream may have work pending that reads or
+ * writes them when the call starts (the caller synchronises its stream first;
+ * the Python host does this for torch tensors). */
 tpt_status tpt_render(tpt_scene* scene, const tpt_env* env, const tpt_camera* camera,
                       const tpt_params* params, float* radiance_out, uint8_t* bgra_out,
                       tpt_stats* stats);

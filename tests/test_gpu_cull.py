@@ -211,3 +211,26 @@ def test_culled_traversal_divergence_is_the_references_rounding(scenes, name, n)
     # shadow rays (any hit) and probes: the same rays, the same bound
     h2, _, _ = d.trace_rays(o, dirs, mode=2)
     assert ((h2 >= 0) != (h0 >= 0)).sum() <= 0.005 * len(o)
+
+
+def test_logged_baseline_divergences_are_fixed(scenes):
+    """The rays of the BASELINE frames on which the culls without the exactness
+    guards lost the reference's hit (tests/golden/cull_regress_rays.json: 4 in
+    C3 -- the ball's sliver triangles, whose Moller-Trumbore t is rounding
+    noise -- and 1 in C5 -- a shared-edge hit a few ulps outside its leaf box,
+    crossed at |d.y| = 1e-3): the render's traversal now finds the reference's
+    hit, in every mode."""
+    import json
+    import os
+    from tests.conftest import ROOT
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "cull_regress_rays.json")))["rays"]
+    for name, rays in gold.items():
+        s, d = scenes[name]
+        f = lambda hs: np.array([int(h, 16) for h in hs], np.uint32).view(np.float32)
+        o = np.stack([f(r["o"]) for r in rays])
+        di = np.stack([f(r["d"]) for r in rays])
+        h0, t0, uv0 = d.trace_rays(o, di, mode=0)
+        assert h0.tolist() == [r["ref_fid"] for r in rays]
+        h1, t1, uv1 = d.trace_rays(o, di, mode=1)
+        assert np.array_equal(h1, h0) and np.array_equal(_bits(t1), _bits(t0)) and np.array_equal(_bits(uv1), _bits(uv0))
+        _check_modes(s, d, o, di, h0, t0, uv0)

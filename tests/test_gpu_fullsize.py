@@ -1,0 +1,78 @@
+"""The BASELINE configurations at their full benchmark sizes,
+checked through size-independent properties (the oracle would need hours):
+
+* the default traversal (nearer child first, culled against the best hit and
+  Delta with the exactness guards of trace.hip "Culling", 4-wide SAH nodes,
+  two-pass probes) renders the same frame bit for bit as the reference's own
+  visit order (TPT_FLAG_REF_ORDER: right child first, no culling, the
+  reference's ternary slab test over its binary LBVH) -- every one of the
+  frame's billions of rays finds the reference's hit (without the guards,
+  TPT_FLAG_APPROX_CULL, 4 rays of C3 and 1 of C5 at 256 spp do not);
+* with delta lights (C3), one lane per pixel and pair mode (a side lane per
+  pixel traces each bounce's shadow rays) render the same frame bit for bit;
+* both traversals trace the same rays (the counts are the reference's);
+* the framebuffer is copyToFB of the radiance: toUChar's truncating clamp of
+  every channel (material.h:74-81), rows flipped, B,G,R order.
+
+C2, C3 and C4 run at their full benchmark size (C2: 9.4 G rays per frame);
+C5 at its full resolution and a quarter of its spp (the reference order is
+several times slower than the default, and the suite has a time budget).
+"""
+import numpy as np
+import pytest
+
+import tinypathtracer_amd as T
+from tests.conftest import scene_path
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+FULL = [
+    # config, scene, W, H, spp, depth, env
+    ("C2", "box", 1920, 1080, 1024, 8, None),
+    ("C3", "ball", 1920, 1080, 4096, 8, "sky"),
+    ("C4", "tir", 1920, 1080, 8192, 32, None),
+    ("C5", "c5", 3840, 2160, 512, 8, None),
+]
+
+
+def _render(pt, d, cam, W, H, spp, depth, **kw):
+    rad = np.zeros((H, W, 3), np.float32)
+    fb = np.zeros((H, W, 4), np.uint8)
+    st = pt.doTrace(d, cam, fb, spp, seed=42, max_depth=depth, radiance=rad, **kw)
+    return rad, fb, st
+
+
+@pytest.mark.parametrize("cfg,name,W,H,spp,depth,env", FULL)
+def test_full_size_default_order_equals_reference_order(cfg, name, W, H, spp, depth, env):
+    s = T.Scene(scene_path(name))
+    d = s.copySceneToDevice(0).build()
+    try:
+        pt = T.PathTracer("", W, H, 0)
+        if env:
+            pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), 0)
+        rad, fb, st = _render(pt, d, s.m_camera, W, H, spp, depth)
+        ref, fbr, str_ = _render(pt, d, s.m_camera, W, H, spp, depth, flags=T._lib.FLAG_REF_ORDER)
+        diff = int((_bits(rad) != _bits(ref)).any(-1).sum())
+        assert diff == 0, (cfg, diff)
+        assert np.array_equal(fb, fbr), cfg
+        assert st["traversals"] == str_["traversals"] and st["shade_hits"] == str_["shade_hits"], cfg
+        if cfg in ("C2", "C4"):   # the culls without the exactness guards (no sliver here; 0 diverging rays)
+            rad3, _, _ = _render(pt, d, s.m_camera, W, H, spp, depth, flags=T._lib.FLAG_APPROX_CULL)
+            assert np.array_equal(_bits(rad3), _bits(rad)), (cfg, "approx cull")
+        if s.lights:   # delta lights: pair mode (the default) against one lane per pixel
+            rad2, fb2, st2 = _render(pt, d, s.m_camera, W, H, spp, depth, lanes_per_pixel=1)
+            assert np.array_equal(_bits(rad2), _bits(rad)), (cfg, "one lane per pixel")
+            assert st2["traversals"] == st["traversals"], cfg
+        # copyToFB (path_tracer.cu:451-471): toUChar truncates, rows top-down, B,G,R
+        assert np.isfinite(rad).all()
+        q = np.clip(rad * np.float32(255.0), 0.0, 255.0).astype(np.uint8)[::-1]
+        assert np.array_equal(fb[..., 0], q[..., 2]) and np.array_equal(fb[..., 1], q[..., 1])
+        assert np.array_equal(fb[..., 2], q[..., 0])
+        assert st["samples"] == W * H * spp
+    finally:
+        d.close()

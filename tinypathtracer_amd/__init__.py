@@ -399,5 +399,11 @@ def _addr(buf):
     if hasattr(buf, "data_ptr"):             # torch tensor (device memory)
         if not buf.is_contiguous():
             raise ValueError("output tensors must be contiguous")
+        if getattr(buf, "is_cuda", False):
+            # the library writes device outputs on its own stream (tpt.h): work the
+            # caller queued on torch's stream (allocation fill, earlier reads) must be
+            # done first
+            import torch
+            torch.cuda.current_stream(buf.device).synchronize()
         return C.c_void_p(buf.data_ptr())
     raise TypeError(f"unsupported buffer type {type(buf)}")

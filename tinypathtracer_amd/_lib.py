@@ -18,6 +18,7 @@ FLAG_NO_COUNTERS = 0x1
 FLAG_REF_ORDER = 0x2
 FLAG_ACCUMULATE = 0x4
 FLAG_ENV_IS = 0x8
+FLAG_APPROX_CULL = 0x10
 
 
 class Material(C.Structure):

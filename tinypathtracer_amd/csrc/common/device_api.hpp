@@ -6,16 +6,17 @@
 //       q2 = (R.min.z, R.max.xyz)  q3 = (bits(left), bits(right), 0, 0)
 //     child ids use the reference numbering (bvh.cu:164-214): id >= F-1 is
 //     the leaf at sorted position id-(F-1).  Bit 30 of every child link is
-//     set when that child's subtree holds an emissive triangle (inner and
-//     inner4); traversals mask it off.
+//     set when that child's subtree holds an emissive triangle; traversals
+//     mask it off.
 //   inner4[8*(F-1)] float4  4-wide nodes for the ordered traversal, numbered
 //     breadth-first: child k box = floats 6k..6k+5 of q0..q5 (min.xyz,
 //     max.xyz), q6 = child ids (-1: none; a 4-wide node id < F-1, or F-1 +
 //     leaf position).  Default (wide_bvh.cpp, host): an SAH tree over the
 //     LBVH's exact leaf boxes in [0, n4), then from emit_root a tree over the
-//     emissive triangles alone.  TPT_WIDE_TREE=lbvh: the LBVH's even-depth
-//     nodes, each holding its up to 4 grandchildren (a leaf child stands for
-//     itself).
+//     emissive triangles alone.  Fallback
+//     (non-finite boxes, or a tree deeper than the stack): the LBVH's
+//     even-depth nodes, each holding its up to 4 grandchildren (a leaf child
+//     stands for itself), bit 30 = emitter (ignored).
 //   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
 //   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, 0), (n2.xyz, 0)
 //   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)
@@ -82,6 +83,10 @@ struct TraceArgs {
     int32_t any_emitter;                 // some triangle emits (else a direct probe adds nothing)
     int32_t emit_root;                   // inner4 id of the emissive-triangle tree (-1: none)
     int32_t emit_inline;                 // that tree is one node of leaves: probe pass 1 in the shading pass
+    const float4* sliver_groups;         // 2 per group: (lo.xyz, first), (hi.xyz, count) (trace.hip "Culling")
+    const float4* sliver_list;           // 2 per sliver: (exact leaf box lo.xyz, position | emissive << 30), (hi.xyz, 0)
+    int32_t n_sliver_groups;             // 0: no sliver triangles
+    float cull_eps;                      // absolute position slack of the t-culls (trace.hip "Culling")
     int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS

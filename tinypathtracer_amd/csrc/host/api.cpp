@@ -26,6 +26,7 @@
 namespace {
 
 thread_local std::string g_last_error;
+constexpr float kInfF = __builtin_huge_valf();
 
 tpt_status fail(tpt_status st, const std::string& msg) {
     g_last_error = msg;
@@ -172,6 +173,10 @@ struct tpt_scene {
     int32_t wide_tree = 0;                  // 1: inner4 holds the SAH 4-wide tree (wide_bvh.cpp)
     int32_t emit_root = -1;                 // inner4 id of the emissive-triangle tree's root (-1: none)
     int32_t emit_inline = 0;                // that tree is one node of leaves (<= 4 emitters)
+    int32_t slivers = 0;                    // sliver triangles (trace.hip "Culling"), re-tested after traversal
+    int32_t n_sliver_groups = 0;
+    DevBuf<float4> sliver_groups, sliver_list;
+    float cull_eps = 0.0f;                  // absolute position slack of the t-culls
     uint32_t tree_depth = 0;
     // inputs
     DevBuf<uint32_t> indices;
@@ -426,14 +431,107 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     s->wide_tree = 0;
     s->emit_root = -1;
     s->emit_inline = 0;
+    s->slivers = 0;
+    s->n_sliver_groups = 0;
+    s->cull_eps = 0.0f;
     if (n > 1 && s->boxes_finite) {
         std::vector<float> lbox(6 * n);
         std::vector<uint32_t> lemit(n);
+        std::vector<float> ltri(12 * n);   // packed leaf triangles (v0, fid), e1, e2 by sorted position
         HIP_OR_FAIL(hipMemcpyAsync(lbox.data(), s->node_box.p + 6 * (n - 1), 6 * n * sizeof(float),
                                    hipMemcpyDeviceToHost, s->stream));
         HIP_OR_FAIL(hipMemcpyAsync(lemit.data(), s->emit.p + (n - 1), n * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    s->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(ltri.data(), s->tri.p, 12 * n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
         HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+        // Culling exactness (trace.hip "Culling"): sliver triangles -- sin of the
+        // angle at v0 between the edges rayHitTriangle uses below 1e-3 -- give
+        // an arbitrary t, so they are listed (in up to 4 groups with union
+        // boxes) and re-tested after every culled traversal; the culls'
+        // absolute position slack is 4 ulps of the largest world coordinate (a
+        // hit point, the next ray's origin, is rounded to its ulp; an edge hit
+        // accepted by barycentric rounding lies a few ulps outside its triangle).
+        std::vector<int> sl;
+        double max_coord = 0.0;
+        for (size_t p = 0; p < n; ++p) {
+            const float* q = &ltri[12 * p];
+            const double a[3] = {q[4], q[5], q[6]}, b[3] = {q[8], q[9], q[10]};
+            const double c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+            const double la = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+            const double lb = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+            const double lc = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+            for (int k = 0; k < 3; ++k)
+                max_coord = std::max(max_coord, std::max(std::fabs((double)q[k]),
+                                                          std::max(std::fabs((double)q[k] + a[k]),
+                                                                   std::fabs((double)q[k] + b[k]))));
+            if (!(lc >= 1e-3 * la * lb) || la == 0.0 || lb == 0.0) sl.push_back((int)p);   // NaN-safe
+        }
+        s->slivers = (int32_t)sl.size();
+        s->cull_eps = 0.0f;
+        if (std::isfinite(max_coord) && max_coord > 0.0) {
+            int ex = 0;
+            (void)std::frexp(max_coord, &ex);                     // max_coord < 2^ex
+            s->cull_eps = (float)std::ldexp(4.0, ex - 24);        // 4 ulps of a float below 2^ex
+        }
+        s->n_sliver_groups = 0;
+        if (!sl.empty()) {
+            // groups 1..: split the list at the median of the longest centroid axis
+            // while a group holds more than 8 slivers and there are < 8 groups;
+            // group 0 is the union of all (tested first by every ray)
+            std::vector<std::pair<int, int>> grp{{0, (int)sl.size()}};
+            auto cen = [&](int p, int k) { return lbox[6 * p + k] + lbox[6 * p + 3 + k]; };
+            for (bool split = true; split && grp.size() < 8;) {
+                split = false;
+                size_t big = 0;
+                for (size_t g = 1; g < grp.size(); ++g)
+                    if (grp[g].second - grp[g].first > grp[big].second - grp[big].first) big = g;
+                const int b0 = grp[big].first, b1 = grp[big].second;
+                if (b1 - b0 <= 8) break;
+                float lo[3] = {kInfF, kInfF, kInfF}, hi[3] = {-kInfF, -kInfF, -kInfF};
+                for (int i = b0; i < b1; ++i)
+                    for (int k = 0; k < 3; ++k) {
+                        lo[k] = std::min(lo[k], cen(sl[i], k));
+                        hi[k] = std::max(hi[k], cen(sl[i], k));
+                    }
+                int ax = 0;
+                for (int k = 1; k < 3; ++k)
+                    if (hi[k] - lo[k] > hi[ax] - lo[ax]) ax = k;
+                const int mid = (b0 + b1) / 2;
+                std::nth_element(sl.begin() + b0, sl.begin() + mid, sl.begin() + b1,
+                                 [&](int x, int y) { return cen(x, ax) < cen(y, ax); });
+                grp[big] = {b0, mid};
+                grp.push_back({mid, b1});
+                split = true;
+            }
+            grp.insert(grp.begin(), {0, (int)sl.size()});   // group 0: the union
+            std::vector<float4> gb(2 * grp.size());
+            std::vector<float4> lst(2 * sl.size());   // exact leaf box, position | emissive << 30
+            for (size_t i = 0; i < sl.size(); ++i) {
+                const int32_t e = sl[i] | (lemit[sl[i]] ? (1 << 30) : 0);
+                float fe;
+                std::memcpy(&fe, &e, 4);
+                const float* b = &lbox[6 * sl[i]];
+                lst[2 * i] = make_float4(b[0], b[1], b[2], fe);
+                lst[2 * i + 1] = make_float4(b[3], b[4], b[5], 0.0f);
+            }
+            for (size_t g = 0; g < grp.size(); ++g) {
+                float lo[3] = {kInfF, kInfF, kInfF}, hi[3] = {-kInfF, -kInfF, -kInfF};
+                for (int i = grp[g].first; i < grp[g].second; ++i)
+                    for (int k = 0; k < 3; ++k) {
+                        lo[k] = std::min(lo[k], lbox[6 * sl[i] + k]);
+                        hi[k] = std::max(hi[k], lbox[6 * sl[i] + 3 + k]);
+                    }
+                int32_t first = grp[g].first, count = grp[g].second - grp[g].first;
+                float ff, fc;
+                std::memcpy(&ff, &first, 4);
+                std::memcpy(&fc, &count, 4);
+                gb[2 * g] = make_float4(lo[0], lo[1], lo[2], ff);
+                gb[2 * g + 1] = make_float4(hi[0], hi[1], hi[2], fc);
+            }
+            HIP_OR_FAIL(s->sliver_groups.upload(gb.data(), gb.size(), s->stream));
+            HIP_OR_FAIL(s->sliver_list.upload(lst.data(), lst.size(), s->stream));
+            s->n_sliver_groups = (int32_t)grp.size();
+        }
         tpt::WideParams prm;
 #ifdef TPT_WIDE_SWEEP
         prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
@@ -573,6 +671,10 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.boxes_finite = s->boxes_finite;
     a.any_emitter = s->any_emitter;
     a.emit_root = s->emit_root;
+    a.sliver_groups = s->sliver_groups.p;
+    a.sliver_list = s->sliver_list.p;
+    a.n_sliver_groups = s->n_sliver_groups;
+    a.cull_eps = s->cull_eps;
 #ifdef TPT_NO_EMIT_INLINE
     a.emit_inline = 0;   // A/B builds: probe pass 1 as a traversal always
 #else
@@ -667,6 +769,10 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     a.n_frames = n_frames;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
+    if (p->flags & TPT_FLAG_APPROX_CULL) {   // culls without the exactness guards (trace.hip "Culling")
+        a.cull_eps = 0.0f;
+        a.n_sliver_groups = 0;
+    }
     // A15 env next-event estimation: opt-in, needs an env with a non-empty distribution
     a.env_is = ((p->flags & TPT_FLAG_ENV_IS) && env && env->is_total > 0.0f) ? 1 : 0;
     a.refill = p->refill > 0 ? std::min(p->refill, 64) : 24;
@@ -727,13 +833,15 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         }
     }
     a.debug_waves = nullptr;
-#ifdef TPT_PROFILE_PHASES
-    const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");   // per-wave dump, phase-profiling builds only
+#if defined(TPT_PROFILE_PHASES) || defined(TPT_VERIFY_CULL)
+    // per-wave dump (phase-profiling builds) / traversal mismatch log (cull-verification builds)
+    const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");
 #else
     const char* dbg_path = nullptr;
 #endif
+    // one record per wave of the largest grid (pair mode: 16x8-pixel workgroups)
     const size_t dbg_launch =
-        8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 15) / 16) * nf;
+        8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 7) / 8) * nf;
     const size_t dbg_words = dbg_launch * std::max<size_t>(plan.size(), 1);   // one region per launch
     if (dbg_path) {
         HIP_OR_FAIL(s->debug.alloc(dbg_words));
@@ -766,6 +874,19 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         for (size_t j = 0; j < order.size(); ++j) order[j] = j;
         std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return t0[x] < t0[y]; });
     }
+    // An error while the sets' launches are being queued must not leave set
+    // streams writing the rng/accumulator planes behind the caller's back (the
+    // next call's reset runs on the main stream): join every set before failing.
+#define SET_OR_FAIL(expr)                                                                                      \
+    do {                                                                                                       \
+        hipError_t e_ = (expr);                                                                                \
+        if (e_ != hipSuccess) {                                                                                \
+            for (int k_ = 0; nset > 1 && k_ < nset; ++k_) (void)hipStreamSynchronize(qs[k_]);                  \
+            (void)hipStreamSynchronize(st);                                                                    \
+            return fail(e_ == hipErrorOutOfMemory ? TPT_ERR_OOM : TPT_ERR_HIP,                                 \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                                    \
+        }                                                                                                      \
+    } while (0)
     for (size_t oi = 0; oi < order.size(); ++oi) {
         const size_t j = order[oi];
         const int k = plan[j].set;
@@ -777,17 +898,22 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
             ak.band_index = p->band_index + k * band_count;
             ak.band_height = set_bh[k];
         }
+#ifdef TPT_VERIFY_CULL
+        if (dbg_path) ak.debug_waves = s->debug.p;   // one log, counters[24] indexes it
+#else
         if (dbg_path) ak.debug_waves = s->debug.p + oi * dbg_launch;
-        HIP_OR_FAIL(hipEventRecord(s->lev[2 * j], qs[k]));
-        HIP_OR_FAIL(tpt::launch_trace(ak, qs[k]));
-        HIP_OR_FAIL(hipEventRecord(s->lev[2 * j + 1], qs[k]));
+#endif
+        SET_OR_FAIL(hipEventRecord(s->lev[2 * j], qs[k]));
+        SET_OR_FAIL(tpt::launch_trace(ak, qs[k]));
+        SET_OR_FAIL(hipEventRecord(s->lev[2 * j + 1], qs[k]));
     }
     for (int k = 0; nset > 1 && k < nset; ++k) {   // join
-        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[1 + k], qs[k]));
-        HIP_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[1 + k], 0));
+        SET_OR_FAIL(hipEventRecord(s->pipe_ev[1 + k], qs[k]));
+        SET_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[1 + k], 0));
     }
-    HIP_OR_FAIL(hipEventRecord(s->ev[2], st));   // end of the trace phase
-    HIP_OR_FAIL(hipEventSynchronize(s->ev[2]));
+    SET_OR_FAIL(hipEventRecord(s->ev[2], st));   // end of the trace phase
+    SET_OR_FAIL(hipEventSynchronize(s->ev[2]));
+#undef SET_OR_FAIL
     double trace_ms = 0.0, kernel_ms = 0.0;
     int launches = 0;
     {
@@ -851,14 +977,20 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     HIP_OR_FAIL(hipStreamSynchronize(st));
     if (cnt[4] != 0) return fail(TPT_ERR_HIP, "traversal stack overflow (BVH deeper than sized)");
     if (dbg_path) {
-        std::vector<unsigned long long> h(dbg_words);
-        HIP_OR_FAIL(hipMemcpy(h.data(), s->debug.p, dbg_words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+#ifdef TPT_VERIFY_CULL
+        const size_t dump_words = std::min<size_t>(dbg_words, 16 * std::min<unsigned long long>(cnt[24], 4096));
+#else
+        const size_t dump_words = dbg_words;
+#endif
+        std::vector<unsigned long long> h(dump_words);
+        if (dump_words)
+            HIP_OR_FAIL(hipMemcpy(h.data(), s->debug.p, dump_words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         if (FILE* f = std::fopen(dbg_path, "wb")) {
             std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
             std::fclose(f);
         }
     }
-#ifdef TPT_PROFILE_PHASES
+#if defined(TPT_PROFILE_PHASES) || defined(TPT_VERIFY_CULL)
     if (std::getenv("TPT_DEBUG_COUNTERS")) {   // raw kernel counters (TPT_PROFILE_PHASES builds: 6..15 phases, 16..22 shading-pass sections)
         std::fprintf(stderr, "tpt counters:");
         for (int i = 0; i < 32; ++i) std::fprintf(stderr, " %llu", cnt[i]);

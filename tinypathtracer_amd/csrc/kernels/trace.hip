@@ -107,11 +107,38 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 // current node is in a register; the LDS stack only holds deferred siblings.
 //  ORDERED == false: the reference's visit order exactly (both children hit ->
 //    right first, left deferred: :95-104), no culling.
-//  ORDERED == true (default): nearer child first; a child is skipped when its
-//    slab entry lies beyond the best hit (1e-4 relative margin) or its exit lies
-//    before Delta/2 -- boxes that cannot hold an accepted hit.  Exact ties
-//    (t == best) resolve to the larger leaf position, the triangle the
-//    reference's right-first DFS meets first, so the winner is the reference's.
+//  ORDERED == true (default): nearer child first; on the 4-wide path a child is
+//    skipped when its slab entry lies beyond the best hit or its exit lies
+//    before Delta/2 -- boxes that cannot hold an accepted hit (Culling, below).
+//    Exact ties (t == best) resolve to the larger leaf position, the triangle
+//    the reference's right-first DFS meets first, so the winner is the
+//    reference's.  The binary path (non-finite rays or boxes) does not cull.
+//
+//  Culling.  The reference tests every leaf whose box the infinite line passes
+//  and keeps the least Moller-Trumbore t > Delta (geometry_queries.h:65-86,
+//  path_tracer.cu:61-107), so a culled box must not hold a triangle whose
+//  *computed* t would win -- and the computed t can lie outside the leaf box's
+//  slab interval:
+//   * sliver triangles (sin of the angle at v0 below 1e-3, e.g. the ball's
+//     zero-area pole triangles): the determinant is rounding noise and t is
+//     arbitrary (measured: a hit at t = 2.15 on a leaf box spanning
+//     [2.89, 2.95]).  The host lists them in up to 8 groups under a union
+//     box; after every culled traversal, sliver_pass tests each sliver whose
+//     exact leaf box the ray's line passes (the reference's rayHitBBox
+//     verdict, no culling) under the same acceptance and tie rules -- exact
+//     for any ray, one box test per ray in scenes with slivers (ball: 54 pole
+//     triangles), nothing otherwise;
+//   * hits on a shared edge accepted by barycentric rounding lie a few ulps
+//     outside the triangle, which is a large t offset when the ray crosses the
+//     box face at a grazing angle (measured: 5e-6 before the box entry at
+//     |d.y| = 1e-3), and a secondary ray's origin lies an ulp off its own
+//     surface: the culls carry an absolute slack of cull_eps (4 ulps of the
+//     largest world coordinate) per unit of max |1/d|, on top of a 1e-4
+//     relative margin for t's own rounding;
+//   * rays grazing a triangle's plane (|cos| < ~1e-4) have the same
+//     ill-conditioned t; origins exactly on an edge or vertex with such
+//     directions diverge at ~1e-3 of adversarial rays (tests/test_gpu_cull.py)
+//     and none of the BASELINE frames' rays (tests/test_gpu_fullsize.py).
 //  Modes:
 //   TM_CLOSEST  closest hit (extension and camera rays; probes in reference order)
 //   TM_ANY      shadow rays stop at the first accepted triangle (only
@@ -135,12 +162,13 @@ struct Trav {
     int node, sp, hpos, fid;
     int pend;   // parked leaf position (speculative traversal), -1: none
     float t, u, v;
-    int mode;   // TM_*
-    bool fin;   // origin and 1/dir finite: no slab product can be NaN
+    float slack;   // absolute t slack of the culls: cull_eps * max |1/d| (Culling)
+    int mode;      // TM_*
+    bool fin;      // origin and 1/dir finite: no slab product can be NaN
 };
 
 __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool boxes_finite = false,
-                                           int emit_root = -1) {
+                                           int emit_root = -1, float cull_eps = 0.0f) {
     r.o = o;
     r.d = d;
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
@@ -155,6 +183,7 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
     r.mode = mode;
     r.fin = boxes_finite & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
             __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
+    r.slack = cull_eps * fmaxf(fmaxf(fabsf(r.inv.x), fabsf(r.inv.y)), fabsf(r.inv.z));
     if (mode == TM_EMIT && r.fin) {
         // probe pass 1 on the 4-wide path walks the emissive-triangle tree; without
         // one it becomes a plain closest-hit probe (the reference's own probe,
@@ -176,14 +205,9 @@ __device__ __forceinline__ void inner_visit(const Trav& r, const float4* __restr
     bool hr = box_hit(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, r0, r1);
     const int lraw = __float_as_int(q3.x), rraw = __float_as_int(q3.y);
     const int lc = lraw & kLinkMask, rc = rraw & kLinkMask;
-    if (ORDERED) {
-        const float lim = r.t * 1.0001f;
-        hl = hl & !(l0 > lim) & !(l1 < 0.5f * kDelta);
-        hr = hr & !(r0 > lim) & !(r1 < 0.5f * kDelta);
-        if (r.mode == TM_EMIT) {   // probe pass 1: emitter subtrees only
-            hl = hl & ((lraw >> 30) != 0);
-            hr = hr & ((rraw >> 30) != 0);
-        }
+    if (ORDERED && r.mode == TM_EMIT) {   // probe pass 1: emitter subtrees only
+        hl = hl & ((lraw >> 30) != 0);
+        hr = hr & ((rraw >> 30) != 0);
     }
     const bool lfirst = ORDERED && (l0 < r0);   // reference order: right child first
     push = hl & hr;
@@ -288,10 +312,10 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
     slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
     slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
-    const float hi = fminf(kRealMax, r.t * 1.0001f);
+    const float hi = fminf(kRealMax, r.t * 1.0001f + r.slack);
     int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z), i3 = __float_as_int(q6.w);
-    const float hd = 0.5f * kDelta;
-    // a link is -1 (no child) or an id with the emitter flag in bit 30
+    const float hd = 0.5f * kDelta - r.slack;
+    // a link is -1 (no child) or an id with a flag in bit 30 (unused here)
     const bool h0 = (i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi));
     const bool h1 = (i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi));
     const bool h2 = (i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi));
@@ -392,13 +416,83 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
     slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
     slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
-    const float hd = 0.5f * kDelta, hi = kRealMax;   // nothing hit yet: r.t = FLT_MAX
+    const float hi = kRealMax;   // nothing hit yet: r.t = FLT_MAX
+    const float hd = 0.5f * kDelta - r.slack;
     const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
               i3 = __float_as_int(q6.w);
     if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint); }
     if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint); }
     if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint); }
     if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint); }
+}
+
+// Slivers (Culling): the triangles the culled traversal cannot be trusted to
+// reach when they matter, re-tested after it against their exact leaf boxes.
+// Group g: sliver_groups[2g] = (lo.xyz, first), [2g + 1] = (hi.xyz, count)
+// over sliver_list, whose entry i is the sliver's exact leaf box (lo.xyz,
+// leaf position | emissive << 30), (hi.xyz, 0) -- no dependent loads; groups
+// 1.. are tested only when the ray passes group 0, the union of all of them.  Finite rays only (the
+// binary path does not cull).  A sliver the traversal already tested is
+// rejected by the tie rule the second time (same t and position).
+// (Out of line and by value: a reference to the lane's traversal state would
+// pin it to scratch memory for the whole kernel.)
+struct SliverHit {
+    float t, u, v;
+    int fid, hpos, mode, tests;
+};
+__device__ __forceinline__ SliverHit sliver_scan(const float4* __restrict__ groups, const float4* __restrict__ list,
+                                              int n_groups, const float4* __restrict__ tri, V3 o, V3 d, V3 inv,
+                                              float slack, SliverHit h) {
+    Trav r;
+    r.o = o;
+    r.d = d;
+    r.inv = inv;
+    r.t = h.t;
+    r.u = h.u;
+    r.v = h.v;
+    r.fid = h.fid;
+    r.hpos = h.hpos;
+    r.mode = h.mode;
+    int tests = 0;
+    float t0, t1;
+    // A sliver whose slab interval [t0, t1] has t1 >= hd and t0 <= lim (the
+    // traversal's final cull bounds) was reached and tested by the traversal
+    // itself; only the others can have been culled.
+    const float hd = 0.5f * kDelta - slack, lim = fminf(kRealMax, h.t * 1.0001f + slack);
+    {
+        const float4 lo = groups[0], hi = groups[1];   // the union box
+        if (!box_hit(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, t0, t1) || (t0 >= hd && t1 <= lim)) n_groups = 0;
+    }
+    for (int g = 1; g < n_groups; ++g) {
+        const float4 lo = groups[2 * g], hi = groups[2 * g + 1];
+        if (!box_hit(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, t0, t1)) continue;
+        const int first = __float_as_int(lo.w), count = __float_as_int(hi.w);
+        bool stop = false;
+        for (int i = first; i < first + count && !stop; ++i) {
+            const float4 bl = list[2 * i], bh = list[2 * i + 1];
+            const int e = __float_as_int(bl.w);
+            if (r.mode == TM_EMIT && !((e >> 30) & 1)) continue;   // probe pass 1: emitters only
+            const int pos = e & kLinkMask;
+            if (!box_hit(o, inv, bl.x, bl.y, bl.z, bh.x, bh.y, bh.z, t0, t1)) continue;   // rayHitBBox
+            if (t1 >= hd && t0 <= lim) continue;   // not culled: already tested
+            ++tests;
+            stop = leaf_test<true>(r, tri, pos);   // any-hit / occluding: done
+        }
+        if (stop) break;
+    }
+    return SliverHit{r.t, r.u, r.v, r.fid, r.hpos, r.mode, tests};
+}
+__device__ __forceinline__ void sliver_pass(Trav& r, const TraceArgs& a, uint32_t& c_leaf) {
+    if (!r.fin || r.mode == TM_OCCLUDED || (r.mode == TM_ANY && r.fid >= 0)) return;
+    const SliverHit h = sliver_scan(a.sliver_groups, a.sliver_list, a.n_sliver_groups, a.tri, r.o, r.d, r.inv, r.slack,
+                                    SliverHit{r.t, r.u, r.v, r.fid, r.hpos, r.mode, 0});
+    r.t = h.t;
+    r.u = h.u;
+    r.v = h.v;
+    r.fid = h.fid;
+    r.hpos = h.hpos;
+    r.mode = h.mode;
+    c_leaf += (uint32_t)h.tests;
 }
 
 __device__ __forceinline__ V3 reflect_dir(V3 d, V3 n) { return d - (2.0f * dot(d, n)) * n; }   // :137-141
@@ -556,6 +650,56 @@ __device__ __noinline__ bool env_is_sample(const TraceArgs& a, V3 nf, uint32_t s
     k_le = k * le;
     return true;
 }
+#ifdef TPT_VERIFY_CULL
+template <bool ORDERED>
+__device__ __forceinline__ void trav_lane(Trav& r, const TraceArgs& a, LaneStack<int>& stk, uint32_t& c_ovf);
+// Diagnostic builds (-DTPT_VERIFY_CULL): every ray the render traversed is traced
+// again in the reference's visit order (no culling) and compared with what the
+// render used -- closest hit (fid, t, u, v bits), shadow verdict, or the probe's
+// emission.  Mismatches go to a.debug_waves, 16 words each, counted in
+// counters[24] (at most kVerifyCap logged).  The image is the render's.
+constexpr unsigned long long kVerifyCap = 4096;
+__device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int phase, const float4* mtl) {
+    Trav q;
+    trav_begin(q, r.o, r.d, TM_CLOSEST);
+    LaneStack<int> vs;
+    vs.lds = nullptr;
+    vs.nlds = 0;
+    uint32_t ovf = 0;
+    trav_lane<false>(q, a, vs, ovf);
+    bool bad;
+    if (r.mode == TM_ANY) {
+        bad = (q.fid >= 0) != (r.fid >= 0);
+    } else if (r.mode == TM_CLOSEST && phase != 3) {
+        bad = (q.fid != r.fid) || (__float_as_uint(q.t) != __float_as_uint(r.t)) ||
+              (__float_as_uint(q.u) != __float_as_uint(r.u)) || (__float_as_uint(q.v) != __float_as_uint(r.v));
+    } else {   // probe: only the closest hit's emission is read (:394-396)
+        const float er = q.fid >= 0 ? mtl[2 * __float_as_int(a.shade[3 * q.fid].w)].w : 0.0f;
+        const float eo = (r.fid >= 0 && r.mode != TM_OCCLUDED) ? mtl[2 * __float_as_int(a.shade[3 * r.fid].w)].w : 0.0f;
+        bad = er != eo;
+    }
+    if (!bad) return;
+    const unsigned long long k = atomicAdd(&a.counters[24], 1ull);
+    if (k >= kVerifyCap || !a.debug_waves) return;
+    unsigned long long* o = a.debug_waves + 16 * k;
+    o[0] = (unsigned long long)r.mode;
+    o[1] = (unsigned long long)phase;
+    o[2] = (unsigned long long)(long long)r.fid;
+    o[3] = (unsigned long long)(long long)q.fid;
+    o[4] = __float_as_uint(r.t);
+    o[5] = __float_as_uint(q.t);
+    o[6] = __float_as_uint(r.o.x);
+    o[7] = __float_as_uint(r.o.y);
+    o[8] = __float_as_uint(r.o.z);
+    o[9] = __float_as_uint(r.d.x);
+    o[10] = __float_as_uint(r.d.y);
+    o[11] = __float_as_uint(r.d.z);
+    o[12] = (unsigned long long)(long long)r.hpos;
+    o[13] = (unsigned long long)(long long)q.hpos;
+    o[14] = __float_as_uint(r.u);
+    o[15] = __float_as_uint(q.u);
+}
+#endif
 // TS_IDLE (pair mode): a side lane without a job, or a path lane waiting for
 // its side lane's direct sum before the unwind -- neither traverses nor shades
 enum : int { TS_DONE = 0, TS_TRAV = 1, TS_DEAD = 2, TS_IDLE = 3 };
@@ -716,6 +860,10 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     Trav r;
     trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), TM_CLOSEST);
     int ts = active ? TS_DONE : ((PAIR && side && pixel) ? TS_IDLE : TS_DEAD);
+#ifdef TPT_VERIFY_CULL
+    bool vpend = false;   // a traversal of this lane awaits verification
+#endif
+    bool sl_pend = false;   // a traversal of this lane awaits the sliver pass
     const int refill = a.refill;
     // pair mode state.  Path lane: partner idle?, the level whose shadow rays the
     // partner holds (-1: none), this level's shadows delegated?, the unwind's seed
@@ -777,6 +925,10 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             t_iter0 = now;
         }
 #endif
+        if (ORDERED && ts == TS_DONE && sl_pend) {   // slivers after a culled traversal (Culling)
+            sl_pend = false;
+            if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
+        }
         if (ORDERED && ts == TS_DONE && phase == PH_PROBE && r.mode == TM_EMIT && r.fid >= 0) {
             // direct probe, pass 2: the emitter hit stands unless something
             // beats it -- restart from the root keeping its t, position and fid
@@ -785,7 +937,14 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             r.sp = 0;
             r.pend = -1;
             ts = TS_TRAV;
+            sl_pend = true;
         }
+#ifdef TPT_VERIFY_CULL
+        if (ts == TS_DONE && vpend) {
+            vpend = false;
+            verify_ray(a, r, phase, a.mtl);
+        }
+#endif
         if (ts == TS_DONE) {
             TPT_SEC_BEGIN()
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
@@ -896,12 +1055,13 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             // <= 4 emitters: pass 1 here; a miss resolves the probe in
                             // this pass, an emitter hit goes on to pass 2 (occlusion)
                             ++c_trav;
-                            trav_begin(r, r.o, td, TM_EMIT, a.boxes_finite != 0, a.emit_root);
+                            trav_begin(r, r.o, td, TM_EMIT, a.boxes_finite != 0, a.emit_root, a.cull_eps);
                             begun = true;
                             phase = PH_PROBE;
                             if (r.mode == TM_EMIT && r.fin) {
                                 ++c_wide;
                                 emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf);
+                                if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
                                 if (r.fid < 0) {
                                     ++c_local;
                                     put_level(kNoProbe, direct);
@@ -1003,9 +1163,13 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 if (!begun) {
                     ++c_trav;
                     trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
-                               a.boxes_finite != 0, a.emit_root);
+                               a.boxes_finite != 0, a.emit_root, a.cull_eps);
                 }
                 ts = TS_TRAV;
+                sl_pend = true;
+#ifdef TPT_VERIFY_CULL
+                vpend = true;
+#endif
             }
             TPT_SEC(6)
         }
@@ -1025,9 +1189,13 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 const V3 jo = v3(jx, jy, jz);
                 light_sample(a.lights, 0, jo, ldir, lrad);
                 ++c_trav;
-                trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root);
+                trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root, a.cull_eps);
                 phase = PH_SHADOW;
                 ts = TS_TRAV;
+                sl_pend = true;
+#ifdef TPT_VERIFY_CULL
+                vpend = true;
+#endif
             }
             post = false;
             // side -> path: the level's direct sum, in light order
@@ -1266,13 +1434,16 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
             fid = r.fid;
         } else {
             const int tm = mode == 1 ? TM_CLOSEST : (mode == 2 ? TM_ANY : TM_EMIT);
-            trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root);
+            trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root, a.cull_eps);
+            uint32_t c_leaf = 0;
             trav_lane<true>(r, a, stk, c_ovf);
+            if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
             if (mode == 3 && r.mode == TM_EMIT && r.fid >= 0) {   // pass 2: does anything beat the emitter hit?
                 r.mode = TM_OCCL;
                 r.node = 0;
                 r.sp = 0;
                 trav_lane<true>(r, a, stk, c_ovf);
+                if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
             }
             fid = (mode == 3 && r.mode == TM_OCCLUDED) ? -2 : r.fid;
             if (mode == 3 && fid >= 0) {   // a closest-hit probe (no emissive tree) may end on a non-emitter
