@@ -775,11 +775,18 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     }
     // A15 env next-event estimation: opt-in, needs an env with a non-empty distribution
     a.env_is = ((p->flags & TPT_FLAG_ENV_IS) && env && env->is_total > 0.0f) ? 1 : 0;
-    a.refill = p->refill > 0 ? std::min(p->refill, 64) : 24;
+
     if (p->lanes_per_pixel < 0 || p->lanes_per_pixel > 2) return fail(TPT_ERR_INVALID_ARG, "lanes_per_pixel: 0, 1 or 2");
     // auto: pair mode wherever there are shadow rays to hand off (C3 1080p 4096 spp:
     // 4.91 -> 6.65 Grays/s); the kernel falls back to one lane per pixel otherwise
     a.pair = (p->lanes_per_pixel == 2 || (p->lanes_per_pixel == 0 && s->n_lights > 0)) ? 1 : 0;
+    // Refill: a wave leaves its traversal loop to shade once fewer than this many
+    // lanes still traverse.  A shading pass costs ~5 node steps, so passes are
+    // batched; in pair mode half the lanes (the side lanes) are mostly idle and
+    // the threshold scales down with them (C3 1080p 4096 spp: 24 -> 5.88,
+    // 8 -> 6.44, 2..12 within 6.2-6.6 Grays/s; C2 single-lane: 16-24 best).
+    const bool pair_kernel = a.pair && s->n_lights > 0 && (s->n_materials + 1) < 0x7fff;
+    a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : 24);
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;

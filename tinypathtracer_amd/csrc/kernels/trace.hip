@@ -131,10 +131,11 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 //   * hits on a shared edge accepted by barycentric rounding lie a few ulps
 //     outside the triangle, which is a large t offset when the ray crosses the
 //     box face at a grazing angle (measured: 5e-6 before the box entry at
-//     |d.y| = 1e-3), and a secondary ray's origin lies an ulp off its own
-//     surface: the culls carry an absolute slack of cull_eps (4 ulps of the
-//     largest world coordinate) per unit of max |1/d|, on top of a 1e-4
-//     relative margin for t's own rounding;
+//     |d.y| = 1e-3): the entry cull carries an absolute slack of cull_eps (4
+//     ulps of the largest world coordinate) per unit of max |1/d|, on top of
+//     a 1e-4 relative margin for t's own rounding.  (The same slack on the
+//     exit cull found no further ray in the verification runs and cost tir
+//     28 %: boxes just behind a secondary ray's origin are entered again.);
 //   * rays grazing a triangle's plane (|cos| < ~1e-4) have the same
 //     ill-conditioned t; origins exactly on an edge or vertex with such
 //     directions diverge at ~1e-3 of adversarial rays (tests/test_gpu_cull.py)
@@ -162,7 +163,7 @@ struct Trav {
     int node, sp, hpos, fid;
     int pend;   // parked leaf position (speculative traversal), -1: none
     float t, u, v;
-    float slack;   // absolute t slack of the culls: cull_eps * max |1/d| (Culling)
+    float slack;   // absolute t slack of the entry cull: cull_eps * max |1/d| (Culling)
     int mode;      // TM_*
     bool fin;      // origin and 1/dir finite: no slab product can be NaN
 };
@@ -314,7 +315,7 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
     slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
     const float hi = fminf(kRealMax, r.t * 1.0001f + r.slack);
     int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z), i3 = __float_as_int(q6.w);
-    const float hd = 0.5f * kDelta - r.slack;
+    const float hd = 0.5f * kDelta;
     // a link is -1 (no child) or an id with a flag in bit 30 (unused here)
     const bool h0 = (i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi));
     const bool h1 = (i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi));
@@ -417,7 +418,7 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
     slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
     slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
     const float hi = kRealMax;   // nothing hit yet: r.t = FLT_MAX
-    const float hd = 0.5f * kDelta - r.slack;
+    const float hd = 0.5f * kDelta;
     const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
               i3 = __float_as_int(q6.w);
     if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint); }
@@ -458,7 +459,7 @@ __device__ __forceinline__ SliverHit sliver_scan(const float4* __restrict__ grou
     // A sliver whose slab interval [t0, t1] has t1 >= hd and t0 <= lim (the
     // traversal's final cull bounds) was reached and tested by the traversal
     // itself; only the others can have been culled.
-    const float hd = 0.5f * kDelta - slack, lim = fminf(kRealMax, h.t * 1.0001f + slack);
+    const float hd = 0.5f * kDelta, lim = fminf(kRealMax, h.t * 1.0001f + slack);
     {
         const float4 lo = groups[0], hi = groups[1];   // the union box
         if (!box_hit(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, t0, t1) || (t0 >= hd && t1 <= lim)) n_groups = 0;
