@@ -89,6 +89,8 @@ def parse():
                     help="tpt_params.lanes_per_pixel: 0 auto, 1, 2 = pair mode (delta-light scenes)")
     ap.add_argument("--pipe-sets", type=int, default=0,
                     help="launch pipeline band sets (tpt_params.pipe_sets): 0 auto, 1 one launch per frame")
+    ap.add_argument("--pipe-chunks", type=int, default=0,
+                    help="spp chunks per band set (tpt_params.pipe_chunks): 0 auto (8)")
     ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
     ap.add_argument("--refill", type=int, default=0, help="0 = library default")
     ap.add_argument("--extra-streams", type=int, default=0,
@@ -351,7 +353,7 @@ def main():
         build_ms.append((time.perf_counter() - tb) * 1e3)
         st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
                               radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
-                              refill=args.refill, pipe_sets=args.pipe_sets,
+                              refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
                               lanes_per_pixel=args.lanes_per_pixel)
         if world == 1:
             return st, radiances[0]

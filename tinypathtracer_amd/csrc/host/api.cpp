@@ -464,7 +464,9 @@ tpt_status tpt_scene_build(tpt_scene* s) {
                 max_coord = std::max(max_coord, std::max(std::fabs((double)q[k]),
                                                           std::max(std::fabs((double)q[k] + a[k]),
                                                                    std::fabs((double)q[k] + b[k]))));
-            if (!(lc >= 1e-3 * la * lb) || la == 0.0 || lb == 0.0) sl.push_back((int)p);   // NaN-safe
+            // (an edge of exactly zero length makes rayHitTriangle's determinant
+            // exactly 0, or NaN with t NaN: never accepted, so not a sliver here)
+            if (la > 0.0 && lb > 0.0 && !(lc >= 1e-3 * la * lb)) sl.push_back((int)p);   // NaN-safe
         }
         s->slivers = (int32_t)sl.size();
         s->cull_eps = 0.0f;

@@ -120,7 +120,9 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 //  *computed* t would win -- and the computed t can lie outside the leaf box's
 //  slab interval:
 //   * sliver triangles (sin of the angle at v0 below 1e-3, e.g. the ball's
-//     zero-area pole triangles): the determinant is rounding noise and t is
+//     near-degenerate cap triangles; one with an edge of exactly zero length
+//     has a determinant of exactly 0 and is never accepted, so it is not one):
+//     the determinant is rounding noise and t is
 //     arbitrary (measured: a hit at t = 2.15 on a leaf box spanning
 //     [2.89, 2.95]).  The host lists them in up to 8 groups under a union
 //     box; after every culled traversal, sliver_pass tests each sliver whose
