@@ -928,10 +928,14 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             t_iter0 = now;
         }
 #endif
-        if (ORDERED && ts == TS_DONE && sl_pend) {   // slivers after a culled traversal (Culling)
-            sl_pend = false;
-            if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
+#ifndef TPT_NO_SLIVERS
+        if (ORDERED && a.n_sliver_groups > 0) {   // (uniform) slivers after a culled traversal (Culling)
+            if (ts == TS_DONE && sl_pend) {
+                sl_pend = false;
+                sliver_pass(r, a, c_leaf);
+            }
         }
+#endif
         if (ORDERED && ts == TS_DONE && phase == PH_PROBE && r.mode == TM_EMIT && r.fid >= 0) {
             // direct probe, pass 2: the emitter hit stands unless something
             // beats it -- restart from the root keeping its t, position and fid
