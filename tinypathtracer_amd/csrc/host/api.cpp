@@ -788,7 +788,14 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // the threshold scales down with them (C3 1080p 4096 spp: 24 -> 5.88,
     // 8 -> 6.44, 2..12 within 6.2-6.6 Grays/s; C2 single-lane: 16-24 best).
     const bool pair_kernel = a.pair && s->n_lights > 0 && (s->n_materials + 1) < 0x7fff;
-    a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : 24);
+    // A launch with fewer pixels than about twice the chip's resident lanes
+    // (256 CUs x 4 SIMDs x 5 waves x 64 = 327,680: strong-scaled frames, small
+    // images) is bound by its heaviest waves' chains, not by throughput: batch
+    // the shading passes harder (C2 rank 0 of 8: refill 24 318 ms, 4: 276 ms;
+    // rank 0 of 4: flat).
+    const double launch_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
+    const bool drained = launch_pix < 2.0 * 327680.0;
+    a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : (drained ? 4 : 24));
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;

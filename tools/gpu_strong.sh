@@ -13,9 +13,3 @@ for n in 1 2 4 8; do
   python -c 'import sys,json; d=json.loads(open(sys.argv[1]).read()); print(sys.argv[2], sys.argv[3], "ms/step", d["ms_per_step"], "trace", d["phases_ms_per_step"]["trace"], "Mrays/s(rank0)", d["value"])' gpurun_out/${TAG}_strong_${C}_$n.json $C $n
 done
 done
-for L in 1 2; do
-  TPT_LIB=$PWD/tinypathtracer_amd/variants/prof/libtpt.so TPT_DEBUG_WAVES=gpurun_out/${TAG}_c3_waves_l$L.bin \
-    timeout -k 10 300 python bench.py --config C3 --spp 512 --pipe-sets 1 --steps 1 --warmup 0 --cpu-baseline 0 \
-    --lanes-per-pixel $L > gpurun_out/${TAG}_c3_prof_l$L.json 2> gpurun_out/${TAG}_c3_prof_l$L.err || { echo "C3 prof $L FAILED"; tail -5 gpurun_out/${TAG}_c3_prof_l$L.err; exit 1; }
-  python tools/wave_timeline.py gpurun_out/${TAG}_c3_waves_l$L.bin $((L == 2 ? 5120 : 5120))
-done
