@@ -1551,7 +1551,10 @@ static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_
 // LDS per 256-lane workgroup: [material table][traversal stack][path records],
 // within kLdsBudget (TPT_TRACE_WAVES workgroups per CU share the 160 KiB).
 constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
-constexpr size_t kLdsMtlMax = 2048;    // material tables up to 64 entries go to LDS
+#ifndef TPT_MTL_LDS_MAX
+#define TPT_MTL_LDS_MAX 2048
+#endif
+constexpr size_t kLdsMtlMax = TPT_MTL_LDS_MAX;   // material tables up to 64 entries go to LDS
 constexpr size_t kLdsNodesMax = TPT_LDS_NODES_MAX;
 
 size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide, int rec_cols = 256) {
