@@ -165,7 +165,7 @@ struct Trav {
     int node, sp, hpos, fid;
     int pend;   // parked leaf position (speculative traversal), -1: none
     float t, u, v;
-    float slack;   // absolute t slack of the entry cull: cull_eps * max |1/d| (Culling)
+    float lim;     // entry-cull bound: min(R, t * 1.0001 + cull_eps * max |1/d|) (Culling), kept with t
     int mode;      // TM_*
     bool fin;      // origin and 1/dir finite: no slab product can be NaN
 };
@@ -186,7 +186,8 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
     r.mode = mode;
     r.fin = boxes_finite & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
             __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
-    r.slack = cull_eps * fmaxf(fmaxf(fabsf(r.inv.x), fabsf(r.inv.y)), fabsf(r.inv.z));
+    r.lim = kRealMax;   // t = FLT_MAX: nothing to cull against yet
+    (void)cull_eps;
     if (mode == TM_EMIT && r.fin) {
         // probe pass 1 on the 4-wide path walks the emissive-triangle tree; without
         // one it becomes a plain closest-hit probe (the reference's own probe,
@@ -315,7 +316,7 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
     slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
     slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
-    const float hi = fminf(kRealMax, r.t * 1.0001f + r.slack);
+    const float hi = r.lim;
     int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z), i3 = __float_as_int(q6.w);
     const float hd = 0.5f * kDelta;
     // a link is -1 (no child) or an id with a flag in bit 30 (unused here)
@@ -386,8 +387,11 @@ __device__ __forceinline__ bool tri_core(const V3& o, const V3& d, const V3& v0,
     return (denom != 0.0f) & !((u < 0.0f) | (v < 0.0f) | (u + v > 1.0f));
 }
 
+__device__ __forceinline__ float cull_slack(const V3& inv, float cull_eps) {
+    return cull_eps * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
+}
 template <bool ORDERED>
-__device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos) {
+__device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos, float cull_eps) {
     const float4* tr = tri + 3 * pos;
     const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
     const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
@@ -396,6 +400,7 @@ __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tr
     const bool better = ORDERED ? ((t < r.t) | ((t == r.t) & (r.hpos >= 0) & (pos > r.hpos))) : (t < r.t);
     const bool take = inside & better & (t > kDelta);   // :83
     r.t = take ? t : r.t;
+    if (ORDERED) r.lim = take ? fminf(kRealMax, t * 1.0001f + cull_slack(r.inv, cull_eps)) : r.lim;
     r.fid = take ? __float_as_int(q0.w) : r.fid;
     r.u = take ? u : r.u;
     r.v = take ? v : r.v;
@@ -412,7 +417,8 @@ __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tr
 // depend on the order the leaves are tested in, so r ends as the traversal
 // would leave it.
 __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restrict__ nd,
-                                                  const float4* __restrict__ tri, int nint, uint32_t& c_leaf) {
+                                                  const float4* __restrict__ tri, int nint, uint32_t& c_leaf,
+                                                  float cull_eps) {
     const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
     float k0, k1, k2, k3, e0, e1, e2, e3;
     slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
@@ -423,10 +429,10 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
     const float hd = 0.5f * kDelta;
     const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
               i3 = __float_as_int(q6.w);
-    if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint); }
-    if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint); }
-    if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint); }
-    if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint); }
+    if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint, cull_eps); }
+    if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint, cull_eps); }
+    if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint, cull_eps); }
+    if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint, cull_eps); }
 }
 
 // Slivers (Culling): the triangles the culled traversal cannot be trusted to
@@ -445,7 +451,7 @@ struct SliverHit {
 };
 __device__ __forceinline__ SliverHit sliver_scan(const float4* __restrict__ groups, const float4* __restrict__ list,
                                               int n_groups, const float4* __restrict__ tri, V3 o, V3 d, V3 inv,
-                                              float slack, SliverHit h) {
+                                              float cull_eps, SliverHit h) {
     Trav r;
     r.o = o;
     r.d = d;
@@ -456,12 +462,13 @@ __device__ __forceinline__ SliverHit sliver_scan(const float4* __restrict__ grou
     r.fid = h.fid;
     r.hpos = h.hpos;
     r.mode = h.mode;
+    r.lim = fminf(kRealMax, h.t * 1.0001f + cull_slack(inv, cull_eps));
     int tests = 0;
     float t0, t1;
     // A sliver whose slab interval [t0, t1] has t1 >= hd and t0 <= lim (the
     // traversal's final cull bounds) was reached and tested by the traversal
     // itself; only the others can have been culled.
-    const float hd = 0.5f * kDelta, lim = fminf(kRealMax, h.t * 1.0001f + slack);
+    const float hd = 0.5f * kDelta, lim = r.lim;
     {
         const float4 lo = groups[0], hi = groups[1];   // the union box
         if (!box_hit(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, t0, t1) || (t0 >= hd && t1 <= lim)) n_groups = 0;
@@ -479,7 +486,7 @@ __device__ __forceinline__ SliverHit sliver_scan(const float4* __restrict__ grou
             if (!box_hit(o, inv, bl.x, bl.y, bl.z, bh.x, bh.y, bh.z, t0, t1)) continue;   // rayHitBBox
             if (t1 >= hd && t0 <= lim) continue;   // not culled: already tested
             ++tests;
-            stop = leaf_test<true>(r, tri, pos);   // any-hit / occluding: done
+            stop = leaf_test<true>(r, tri, pos, cull_eps);   // any-hit / occluding: done
         }
         if (stop) break;
     }
@@ -487,7 +494,7 @@ __device__ __forceinline__ SliverHit sliver_scan(const float4* __restrict__ grou
 }
 __device__ __forceinline__ void sliver_pass(Trav& r, const TraceArgs& a, uint32_t& c_leaf) {
     if (!r.fin || r.mode == TM_OCCLUDED || (r.mode == TM_ANY && r.fid >= 0)) return;
-    const SliverHit h = sliver_scan(a.sliver_groups, a.sliver_list, a.n_sliver_groups, a.tri, r.o, r.d, r.inv, r.slack,
+    const SliverHit h = sliver_scan(a.sliver_groups, a.sliver_list, a.n_sliver_groups, a.tri, r.o, r.d, r.inv, a.cull_eps,
                                     SliverHit{r.t, r.u, r.v, r.fid, r.hpos, r.mode, 0});
     r.t = h.t;
     r.u = h.u;
@@ -495,6 +502,7 @@ __device__ __forceinline__ void sliver_pass(Trav& r, const TraceArgs& a, uint32_
     r.fid = h.fid;
     r.hpos = h.hpos;
     r.mode = h.mode;
+    r.lim = fminf(kRealMax, r.t * 1.0001f + cull_slack(r.inv, a.cull_eps));
     c_leaf += (uint32_t)h.tests;
 }
 
@@ -1067,7 +1075,8 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                             phase = PH_PROBE;
                             if (r.mode == TM_EMIT && r.fin) {
                                 ++c_wide;
-                                emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf);
+                                emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf,
+                                                  a.cull_eps);
                                 if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
                                 if (r.fid < 0) {
                                     ++c_local;
@@ -1283,7 +1292,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                                 __ballot(inner_ready) == 0ull;
                 if (go && has) {
                     ++c_leaf;
-                    if (leaf_test<ORDERED>(r, a.tri, r.pend)) {
+                    if (leaf_test<ORDERED>(r, a.tri, r.pend, a.cull_eps)) {
                         r.node = -1;
                         r.sp = 0;
                     }
@@ -1416,7 +1425,7 @@ __device__ __forceinline__ void trav_lane(Trav& r, const TraceArgs& a, LaneStack
             }
             r.node = next >= 0 ? next : (r.sp == 0 ? -1 : stk.get(--r.sp));
         } else {
-            const bool stop = leaf_test<ORDERED>(r, a.tri, r.node - nint);
+            const bool stop = leaf_test<ORDERED>(r, a.tri, r.node - nint, a.cull_eps);
             r.node = (stop || r.sp == 0) ? -1 : stk.get(--r.sp);
         }
     }
