@@ -880,9 +880,10 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     // partner holds (-1: none), this level's shadows delegated?, the unwind's seed
     // while waiting for the partner, a job to post at the next exchange.  Side
     // lane: the level it works on and the direct sum it hands back.
-    bool p_idle = true, delegated = false, post = false, ready = false;
+    bool delegated = false, post = false, ready = false;   // (partner idle <=> pend < 0)
     int pend = -1, jlevel = 0;
-    V3 Lwait = v3(0.0f, 0.0f, 0.0f);
+    // (the unwind's seed while the path lane waits for its side lane lives in
+    // `direct`: the path's levels are all recorded by then)
     // a level's record: pm = the material the probe hit (kNoProbe: none), dl =
     // its direct term (delta lights + probe emission).  Pair mode keeps the
     // probe symbolic and the delta lights' sum apart (the side lane may still be
@@ -1014,19 +1015,18 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 put_level(pm, dl);
                 after = true;
             } else if (PAIR && phase == PH_WAIT) {   // the side lane's direct sum has arrived
-                L = Lwait;
+                L = direct;
                 finish = true;
             }
             TPT_SEC(1)
             V3 td = rd;
             bool shadow = false;
-            if (PAIR && lights_next && !side && li == 0 && p_idle) {
+            if (PAIR && lights_next && !side && li == 0 && pend < 0) {
                 // hand this bounce's shadow rays to the idle side lane (posted at the
                 // exchange below: origin r.o, material mk, level depth)
                 post = true;
                 jlevel = depth;
                 pend = depth;
-                p_idle = false;
                 delegated = true;
                 li = a.n_lights;
             }
@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             TPT_SEC(3)
             if (PAIR && finish && pend >= 0) {
                 // the side lane still sums a level's shadow rays: wait for it (exchange below)
-                Lwait = L;
+                direct = L;
                 phase = PH_WAIT;
                 ts = TS_IDLE;
                 finish = false;
@@ -1224,7 +1224,6 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 rec.put(rl, 3, dy);
                 rec.put(rl, 4, dz);
                 pend = -1;
-                p_idle = true;
                 if (phase == PH_WAIT) ts = TS_DONE;
             }
             ready = false;
