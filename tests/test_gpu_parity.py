@@ -144,6 +144,7 @@ CASES = [
     ("light", 64, 36, 8, 8, "sky"),
     ("box1", 40, 24, 8, 8, "sky"),
     ("c5", 96, 54, 8, 8, None),   # 131,712 triangles: 32-bit stack ids, LDS + private stack
+    ("c5", 256, 40, 2, 8, None),  # 16 tiles per row: XCD runs of 2 (k_trace prologue)
 ]
 
 

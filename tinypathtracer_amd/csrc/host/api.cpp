@@ -800,6 +800,17 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // 84.6 Grays/s vs 24 72.6-78.9; box (1,932) 16 = 24; C5 (131 K) 16 -3 %.
     const int full = s->n_faces <= 4096 ? 16 : 24;
     a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : (drained ? 4 : full));
+    // XCD runs (trace.hip k_trace prologue) for scenes that do not fit one XCD's
+    // 4 MiB L2 (≈ 200 B of nodes, triangles and shading data per face): the
+    // largest run length <= 10 that divides a row's tiles per XCD (C5 3840 px:
+    // 10 +4.1 %, 30 +3.7 %, 5 +2.1 %, 3 +1.9 %).
+    a.xcd_run = 0;
+    if (s->n_faces > 16384) {
+        const int gx = (W + 15) / 16, per = gx / 8;
+        if (gx % 8 == 0)
+            for (int g = std::min(per, 10); g >= 2 && a.xcd_run == 0; --g)
+                if (per % g == 0) a.xcd_run = g;
+    }
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;

@@ -796,13 +796,25 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     // same screen rows of successive frames, so the resident tiles keep the
     // screen locality of a single frame (node reuse in L1/L2)
     const int nfr = a.n_frames > 0 ? a.n_frames : 1;
-    const int frame = (int)blockIdx.y % nfr;
+    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    // XCD runs (scenes larger than an XCD's 4 MiB L2): blocks b and b + 8 share
+    // an XCD.  Within each row of workgroups XCD k gets runs of xcd_run
+    // adjacent tiles instead of every 8th tile, so its resident tiles see less
+    // of the scene; the run-to-XCD assignment rotates by one every row so every
+    // XCD gets every column over the launch (a permutation of the row's tiles;
+    // the host checks that xcd_run divides gridDim.x / 8).  C5 +4 %; on box,
+    // whose scene is L2-resident anyway, runs cost 2-7 % (the heavy middle
+    // columns then load fewer XCDs), so it stays off there.
+    if (a.xcd_run > 0) {
+        const int g = a.xcd_run, k = ((bx & 7) + by) & 7, m = bx >> 3;
+        bx = ((m / g) * 8 + k) * g + m % g;
+    }
+    const int frame = by % nfr;
     // pair mode: lane 2q (path) and 2q + 1 (side) serve pixel q of the wave's 8x4 tile
     const bool side = PAIR && (lane & 1);
     const int pl = PAIR ? (lane >> 1) : lane;   // pixel slot in the wave
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (pl & 7);
-    const int ly = PAIR ? ((int)blockIdx.y / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3)
-                        : ((int)blockIdx.y / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
+    const int x = bx * 16 + (wave & 1) * 8 + (pl & 7);
+    const int ly = PAIR ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3) : (by / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
     const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
     const bool pixel = x < a.width && ly < a.band_height && y < a.height;
     const bool active = pixel && !side;   // owns the pixel's RNG stream and sums
@@ -1609,6 +1621,8 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
     dim3 grid((a.width + 15) / 16, ((a.band_height + 15) / 16) * (a.n_frames > 0 ? a.n_frames : 1));
+    // the XCD-run remap is a permutation of a row's tiles only if runs tile gridDim.x / 8
+    if (a.xcd_run > 0 && (grid.x % 8 != 0 || (grid.x / 8) % (unsigned)a.xcd_run != 0)) a.xcd_run = 0;
     if (a.flags & TPT_FLAG_REF_ORDER) {
         // the reference's visit order (tests, diagnostics): one general variant
         const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, false);
