@@ -93,6 +93,7 @@ def parse():
                     help="spp chunks per band set (tpt_params.pipe_chunks): 0 auto (8)")
     ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
     ap.add_argument("--refill", type=int, default=0, help="0 = library default")
+    ap.add_argument("--leaf-batch", type=int, default=0, help="tpt_params.leaf_batch: 0 = library default")
     ap.add_argument("--extra-streams", type=int, default=0,
                     help="diagnostic: create this many busy-once HIP streams before the scene (as a process "
                          "group's communicator streams would), to check the launch pipeline's queue use")
@@ -354,7 +355,7 @@ def main():
         st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
                               radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
                               refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
-                              lanes_per_pixel=args.lanes_per_pixel)
+                              lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch)
         if world == 1:
             return st, radiances[0]
         src = radiances if args.dist_backend == "nccl" else [r.cpu() for r in radiances]   # gloo: host tensors

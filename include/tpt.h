@@ -107,6 +107,10 @@ typedef struct {
      * sample's serial chain pays one traversal per bounce.
      * Bit-identical either way. */
     int32_t lanes_per_pixel;
+    /* 0 = auto: a wave runs its parked triangle tests once this many lanes are blocked on
+     * a parked leaf (speculative leaf postponement): 2 in pair mode,
+     * else 4.  Bit-identical for any value. */
+    int32_t leaf_batch;
 } tpt_params;
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */

@@ -312,7 +312,7 @@ class PathTracer:
     def doTrace(self, d_scene: DeviceScene, camera: Camera, framebuffer=None, nSamplesPerPixel: int = 64,
                 seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
                 flags: int = 0, refill: int = 0, accumulate: bool = False, pipe_sets: int = 0,
-                pipe_chunks: int = 0, lanes_per_pixel: int = 0):
+                pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0):
         """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
         or torch CUDA tensors / raw device pointers (device, int).
         accumulate=True: progressive rendering (TPT_FLAG_ACCUMULATE) -- continue
@@ -329,7 +329,7 @@ class PathTracer:
             seed = int(time.time())
         self._last_seed = seed
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags,
-                        refill, pipe_sets, pipe_chunks, lanes_per_pixel)
+                        refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
         rad_p = _addr(radiance)
@@ -341,7 +341,7 @@ class PathTracer:
     def doTraceFrames(self, d_scene: DeviceScene, camera: Camera, seeds, framebuffers=None,
                       nSamplesPerPixel: int = 64, max_depth: int = 8, radiances=None, band=(16, 1, 0),
                       spp_per_launch: int = 0, flags: int = 0, refill: int = 0, accumulate: bool = False,
-                      pipe_sets: int = 0, pipe_chunks: int = 0, lanes_per_pixel: int = 0):
+                      pipe_sets: int = 0, pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0):
         """A batch of independent frames in one trace launch (tpt_render_frames):
         frame f is doTrace(..., seed=seeds[f]) bit for bit.  framebuffers /
         radiances: None or one buffer (or None) per frame."""
@@ -355,7 +355,7 @@ class PathTracer:
             flags |= _lib.FLAG_ACCUMULATE
         W, H = self.m_width, self.m_height
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seeds[0], band[0], band[1], band[2], spp_per_launch,
-                        flags, refill, pipe_sets, pipe_chunks, lanes_per_pixel)
+                        flags, refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
 

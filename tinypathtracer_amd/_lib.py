@@ -57,7 +57,7 @@ class Params(C.Structure):
                 ("seed", C.c_uint64), ("band_rows", C.c_int32), ("band_count", C.c_int32),
                 ("band_index", C.c_int32), ("spp_per_launch", C.c_int32), ("flags", C.c_int32),
                 ("refill", C.c_int32), ("pipe_sets", C.c_int32), ("pipe_chunks", C.c_int32),
-                ("lanes_per_pixel", C.c_int32)]
+                ("lanes_per_pixel", C.c_int32), ("leaf_batch", C.c_int32)]
 
 
 class Stats(C.Structure):

@@ -79,6 +79,7 @@ struct TraceArgs {
     int32_t samples;                     // samples for this launch
     int32_t flags;
     int32_t refill;                      // leave the traversal loop below this many active lanes
+    int32_t leaf_kb;                     // run the parked triangle tests once this many lanes are blocked
     int32_t boxes_finite;                // all node boxes finite: min/max slab test is exact
     int32_t any_emitter;                 // some triangle emits (else a direct probe adds nothing)
     int32_t emit_root;                   // inner4 id of the emissive-triangle tree (-1: none)

@@ -800,6 +800,12 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // 84.6 Grays/s vs 24 72.6-78.9; box (1,932) 16 = 24; C5 (131 K) 16 -3 %.
     const int full = s->n_faces <= 4096 ? 16 : 24;
     a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : (drained ? 4 : full));
+    // Parked-leaf batch (speculative leaf postponement): a wave runs its triangle
+    // tests once this many lanes are blocked on a parked leaf.  Pair mode has
+    // half the path lanes and its heavy waves few traversing lanes, so it
+    // batches less (C3 4096 spp: 4 -> 6.84, 2 -> 7.45, 8 -> 5.86 Grays/s;
+    // C2 and C5 within 2 % either way).
+    a.leaf_kb = p->leaf_batch > 0 ? std::min(p->leaf_batch, 64) : (pair_kernel ? 2 : 4);
     // XCD runs (trace.hip k_trace prologue) for scenes that do not fit one XCD's
     // 4 MiB L2 (≈ 200 B of nodes, triangles and shading data per face): the
     // largest run length <= 10 that divides a row's tiles per XCD (C5 3840 px:

@@ -39,11 +39,8 @@
 #ifndef TPT_PROBE_SHORTCUT
 #define TPT_PROBE_SHORTCUT 1   // no emissive triangle: resolve direct probes in the shading pass
 #endif
-#ifndef TPT_LEAF_KB
-#define TPT_LEAF_KB 4     // run the triangle branch once this many lanes are blocked ...
-#endif
 #ifndef TPT_LEAF_KP
-#define TPT_LEAF_KP 24    // ... or this many lanes hold a parked leaf
+#define TPT_LEAF_KP 24    // run the triangle branch once this many lanes hold a parked leaf (or a.leaf_kb are blocked)
 #endif
 // Top 4-wide nodes staged in LDS (breadth-first prefix of inner4).  Off by
 // default: measured on box 256 spp, 14 staged nodes cost 10 % (the per-visit
@@ -1299,7 +1296,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             }
             const unsigned long long hb = __ballot(has);
             if (hb != 0ull) {
-                const bool go = __popcll(__ballot(blocked)) >= TPT_LEAF_KB || __popcll(hb) >= TPT_LEAF_KP ||
+                const bool go = __popcll(__ballot(blocked)) >= a.leaf_kb || __popcll(hb) >= TPT_LEAF_KP ||
                                 __ballot(inner_ready) == 0ull;
                 if (go && has) {
                     ++c_leaf;
