@@ -804,7 +804,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // tests once this many lanes are blocked on a parked leaf.  Pair mode has
     // half the path lanes and its heavy waves few traversing lanes, so it
     // batches less (C3 4096 spp: 4 -> 6.84, 2 -> 7.45, 8 -> 5.86 Grays/s;
-    // C2 and C5 within 2 % either way).
+    // C2, C4 and C5 within 2 % either way).
     a.leaf_kb = p->leaf_batch > 0 ? std::min(p->leaf_batch, 64) : (pair_kernel ? 2 : 4);
     // XCD runs (trace.hip k_trace prologue) for scenes that do not fit one XCD's
     // 4 MiB L2 (≈ 200 B of nodes, triangles and shading data per face): the

@@ -13,9 +13,10 @@
 //    traversal state in registers -- the wave pays the average traversal length
 //    of its lanes, not the longest, and every pixel still consumes its own
 //    XORWOW stream in the reference's order;
-//  * ordered traversal over 4-wide nodes (the even-depth nodes of the binary
-//    LBVH, 128 B: seven 16-B loads per visit) with an exact min/max slab test
-//    for finite rays, and speculative leaf postponement; the binary nodes and
+//  * ordered traversal over 4-wide nodes (an SAH tree over the reference's
+//    exact leaf boxes, host/wide_bvh.cpp; 128 B: seven 16-B loads per visit)
+//    with an exact min/max slab test for finite rays, the exactness guards of
+//    "Culling" below, and speculative leaf postponement; the binary nodes and
 //    the reference's ternary slab test serve the reference visit order and
 //    rays with a non-finite origin or 1/dir;
 //  * LDS per workgroup: the material table, the traversal stack ([slot][lane],
