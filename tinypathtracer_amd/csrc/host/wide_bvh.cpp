@@ -22,6 +22,7 @@
 #include <array>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "tpt_internal.hpp"
@@ -74,26 +75,41 @@ struct Builder {
         return b;
     }
 
+    // Stable insertion sort of v[0, m) by centroid coordinate `axis`: the same
+    // order as std::stable_sort, without its buffer (m <= sweep_max is small).
+    void sort_axis(int* v, int m, int axis) const {
+        for (int i = 1; i < m; ++i) {
+            const int x = v[i];
+            const float kx = cen[3 * x + axis];
+            int j = i;
+            for (; j > 0 && kx < cen[3 * v[j - 1] + axis]; --j) v[j] = v[j - 1];
+            v[j] = x;
+        }
+    }
+
     // Splits idx[b, e) in place; returns the split point (b < m < e).
     int split(int b, int e) {
         const int m = e - b;
-        Box cb;
-        cb.empty();
-        for (int i = b; i < e; ++i)
-            for (int k = 0; k < 3; ++k) {
-                cb.lo[k] = std::min(cb.lo[k], cen[3 * idx[i] + k]);
-                cb.hi[k] = std::max(cb.hi[k], cen[3 * idx[i] + k]);
-            }
         double best = __builtin_inf();
         int best_axis = -1, best_m = -1;
         if (m <= sweep_max) {
-            // exact sweep over sorted centroids on each axis
-            std::vector<int> tmp(idx.begin() + b, idx.begin() + e);
-            std::vector<double> right_area(m);
+            // exact sweep over sorted centroids on each axis (each axis sorts the
+            // previous axis's order, ties keep it; the range itself is then sorted
+            // from its own order by the chosen axis)
+            constexpr int kLocal = 64;
+            int tmp_l[kLocal];
+            double ra_l[kLocal];
+            std::vector<int> tmp_v;
+            std::vector<double> ra_v;
+            if (m > kLocal) {
+                tmp_v.resize(m);
+                ra_v.resize(m);
+            }
+            int* tmp = m > kLocal ? tmp_v.data() : tmp_l;
+            double* right_area = m > kLocal ? ra_v.data() : ra_l;
+            std::copy(idx.begin() + b, idx.begin() + e, tmp);
             for (int axis = 0; axis < 3; ++axis) {
-                std::stable_sort(tmp.begin(), tmp.end(), [&](int x, int y) {
-                    return cen[3 * x + axis] < cen[3 * y + axis];
-                });
+                sort_axis(tmp, m, axis);
                 Box acc;
                 acc.empty();
                 for (int i = m - 1; i > 0; --i) {
@@ -111,41 +127,61 @@ struct Builder {
                     }
                 }
             }
-            std::stable_sort(idx.begin() + b, idx.begin() + e, [&](int x, int y) {
-                return cen[3 * x + best_axis] < cen[3 * y + best_axis];
-            });
+            if (best_axis < 0) {   // no finite cost (NaN boxes): halve by position
+                std::sort(idx.begin() + b, idx.begin() + e);
+                return b + m / 2;
+            }
+            sort_axis(idx.data() + b, m, best_axis);
             return b + best_m;
         }
+        Box cb;
+        cb.empty();
+        for (int i = b; i < e; ++i)
+            for (int k = 0; k < 3; ++k) {
+                cb.lo[k] = std::min(cb.lo[k], cen[3 * idx[i] + k]);
+                cb.hi[k] = std::max(cb.hi[k], cen[3 * idx[i] + k]);
+            }
         constexpr int kBins = 32;
+        // one pass bins every axis (each leaf's box and centroid read once)
+        Box bb[3][kBins];
+        int bn[3][kBins] = {};
+        float scl[3];
+        bool live[3];
         for (int axis = 0; axis < 3; ++axis) {
             const float ext = cb.hi[axis] - cb.lo[axis];
-            if (!(ext > 0.0f)) continue;
-            Box bb[kBins];
-            int bn[kBins] = {};
-            for (auto& x : bb) x.empty();
-            const float sc = kBins / ext;
-            for (int i = b; i < e; ++i) {
-                int k = (int)((cen[3 * idx[i] + axis] - cb.lo[axis]) * sc);
+            live[axis] = ext > 0.0f;
+            scl[axis] = kBins / ext;
+            for (auto& x : bb[axis]) x.empty();
+        }
+        for (int i = b; i < e; ++i) {
+            const int p = idx[i];
+            const Box lb = leaf_box(p);
+            for (int axis = 0; axis < 3; ++axis) {
+                if (!live[axis]) continue;
+                int k = (int)((cen[3 * p + axis] - cb.lo[axis]) * scl[axis]);
                 k = std::min(std::max(k, 0), kBins - 1);
-                ++bn[k];
-                bb[k].grow(leaf_box(idx[i]));
+                ++bn[axis][k];
+                bb[axis][k].grow(lb);
             }
+        }
+        for (int axis = 0; axis < 3; ++axis) {
+            if (!live[axis]) continue;
             double ra[kBins];
             int rn[kBins];
             Box acc;
             acc.empty();
             int cnt = 0;
             for (int k = kBins - 1; k > 0; --k) {
-                acc.grow(bb[k]);
-                cnt += bn[k];
+                acc.grow(bb[axis][k]);
+                cnt += bn[axis][k];
                 ra[k] = acc.area();
                 rn[k] = cnt;
             }
             acc.empty();
             cnt = 0;
             for (int k = 1; k < kBins; ++k) {
-                acc.grow(bb[k - 1]);
-                cnt += bn[k - 1];
+                acc.grow(bb[axis][k - 1]);
+                cnt += bn[axis][k - 1];
                 if (cnt == 0 || rn[k] == 0) continue;
                 const double c = acc.area() * cnt + ra[k] * rn[k];
                 if (c < best) {
@@ -160,35 +196,56 @@ struct Builder {
             return b + m / 2;
         }
         const float sc = kBins / (cb.hi[best_axis] - cb.lo[best_axis]);
-        auto mid = std::stable_partition(idx.begin() + b, idx.begin() + e, [&](int p) {
+        // stable partition: bins < best_m first, both sides in their order
+        auto left_of = [&](int p) {
             int k = (int)((cen[3 * p + best_axis] - cb.lo[best_axis]) * sc);
             k = std::min(std::max(k, 0), kBins - 1);
             return k < best_m;
-        });
-        int s = (int)(mid - idx.begin());
+        };
+        thread_local std::vector<int> right;
+        right.clear();
+        int s = b;
+        for (int i = b; i < e; ++i) {
+            const int p = idx[i];
+            if (left_of(p)) idx[s++] = p;
+            else right.push_back(p);
+        }
+        std::copy(right.begin(), right.end(), idx.begin() + s);
         if (s == b || s == e) s = b + m / 2;
         return s;
     }
 
-    int build(int b, int e, const uint32_t* emit) {
-        const int id = (int)nodes.size();
-        nodes.emplace_back();
+    // Builds idx[b, e) as the subtree rooted at nodes[id].  Every leaf holds one
+    // triangle, so a subtree of m leaves has 2m - 1 nodes and its pre-order ids
+    // are known before it is built: the left child is id + 1, the right child
+    // id + 2 * (left leaves).  Large left subtrees therefore build on their own
+    // thread straight into the shared array (disjoint idx ranges and node ids),
+    // and the tree is identical to a serial build's.
+    void build(int b, int e, int id, const uint32_t* emit, int spawn) {
+        BNode& nd = nodes[id];
         if (e - b == 1) {
-            nodes[id].pos = idx[b];
-            nodes[id].box = leaf_box(idx[b]);
-            nodes[id].emit = emit[idx[b]] ? 1u : 0u;
-            return id;
+            nd.pos = idx[b];
+            nd.box = leaf_box(idx[b]);
+            nd.emit = emit[idx[b]] ? 1u : 0u;
+            return;
         }
         const int s = split(b, e);
-        const int l = build(b, s, emit);
-        const int r = build(s, e, emit);
-        nodes[id].left = l;
-        nodes[id].right = r;
-        nodes[id].box = nodes[l].box;
-        nodes[id].box.grow(nodes[r].box);
-        nodes[id].emit = nodes[l].emit | nodes[r].emit;
-        return id;
+        const int l = id + 1, r = id + 2 * (s - b);
+        if (spawn > 0 && s - b >= kParMin && e - s >= kParMin) {
+            std::thread t([&, b, s, l] { build(b, s, l, emit, spawn - 1); });
+            build(s, e, r, emit, spawn - 1);
+            t.join();
+        } else {   // (a lopsided split keeps its threads for the larger side)
+            build(b, s, l, emit, spawn);
+            build(s, e, r, emit, spawn);
+        }
+        nd.left = l;
+        nd.right = r;
+        nd.box = nodes[l].box;
+        nd.box.grow(nodes[r].box);
+        nd.emit = nodes[l].emit | nodes[r].emit;
     }
+    static constexpr int kParMin = 4096;   // smallest subtree worth a thread
 };
 
 }  // namespace
@@ -215,8 +272,13 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
     B.cen.resize(3 * (size_t)(pmax + 1));
     for (int p : pos)
         for (int k = 0; k < 3; ++k) B.cen[3 * p + k] = 0.5f * (leaf_box[6 * p + k] + leaf_box[6 * p + 3 + k]);
-    B.nodes.reserve(2 * (size_t)n);
-    const int root = B.build(0, n, leaf_emit);
+    B.nodes.assign(2 * (size_t)n - 1, BNode{});
+    // threads: up to 2^spawn concurrent subtrees, bounded by the cores this process may use
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    int spawn = 0;
+    while (spawn < 5 && (2u << spawn) <= hw) ++spawn;
+    const int root = 0;
+    B.build(0, n, root, leaf_emit, spawn);
     const auto& N = B.nodes;
     if (N[root].left < 0) {   // a single leaf: one node holding it
         out.assign(32, 0.0f);
