@@ -227,6 +227,7 @@ struct Builder {
             nd.pos = idx[b];
             nd.box = leaf_box(idx[b]);
             nd.emit = emit[idx[b]] ? 1u : 0u;
+            collapse_cost(id);
             return;
         }
         const int s = split(b, e);
@@ -244,71 +245,19 @@ struct Builder {
         nd.box = nodes[l].box;
         nd.box.grow(nodes[r].box);
         nd.emit = nodes[l].emit | nodes[r].emit;
+        collapse_cost(id);
     }
     static constexpr int kParMin = 4096;   // smallest subtree worth a thread
-};
 
-}  // namespace
-
-// Leaves: the LBVH sorted positions `pos` (all of them, or a subset such as the
-// emissive triangles); leaf_box[6 * p] / leaf_emit[p] by position p.  Writes 32
-// floats per 4-wide node in the inner4 layout of device_api.hpp (breadth-first,
-// root first; child links: id_base + a node's index, or leaf_base + position
-// for a leaf, with the emitter flag in bit 30; -1 none) and returns the node
-// count; *stack_need = the most stack entries the ordered 4-wide walk can hold
-// right after a visit (trace.hip inner_visit4; see below).
-int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
-                   int id_base, std::vector<float>& out, int* stack_need, const WideParams& prm) {
-    const int n = (int)pos.size();
-    out.clear();
-    *stack_need = 0;
-    if (n == 0) return 0;
-    Builder B;
-    B.lbox = leaf_box;
-    B.sweep_max = prm.sweep_max;
-    B.idx = pos;
-    int pmax = 0;
-    for (int p : pos) pmax = std::max(pmax, p);
-    B.cen.resize(3 * (size_t)(pmax + 1));
-    for (int p : pos)
-        for (int k = 0; k < 3; ++k) B.cen[3 * p + k] = 0.5f * (leaf_box[6 * p + k] + leaf_box[6 * p + 3 + k]);
-    B.nodes.assign(2 * (size_t)n - 1, BNode{});
-    // threads: up to 2^spawn concurrent subtrees, bounded by the cores this process may use
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    int spawn = 0;
-    while (spawn < 5 && (2u << spawn) <= hw) ++spawn;
-    const int root = 0;
-    B.build(0, n, root, leaf_emit, spawn);
-    const auto& N = B.nodes;
-    if (N[root].left < 0) {   // a single leaf: one node holding it
-        out.assign(32, 0.0f);
-        for (int j = 0; j < 3; ++j) {
-            out[j] = N[root].box.lo[j];
-            out[3 + j] = N[root].box.hi[j];
-        }
-        const int32_t links[4] = {(leaf_base + N[root].pos) | (int32_t)(N[root].emit << 30), -1, -1, -1};
-        std::memcpy(out.data() + 24, links, sizeof links);
-        *stack_need = 0;
-        return 1;
-    }
-
-    // Collapse to 4-wide nodes by dynamic programming over the binary tree
-    // (the SAH cost of Ylitie et al. 2017's wide-BVH collapse, 1 triangle per
-    // leaf): D[x][k] is the least cost of representing subtree x as a forest
-    // of at most k subtrees.  Every leaf is some node's child exactly once, so
-    // its triangle-test cost (area-weighted) is the same in every collapse and
-    // drops out; a subtree kept whole costs its area (the probability that its
-    // 4-wide node is visited) plus the best 4-way forest of its children.
-    // Greedy opening of the largest child leaves the bottom levels with 2-leaf
-    // nodes; the DP pulls leaves up into their grandparents.
-    const size_t nb = N.size();
-    std::vector<std::array<double, 5>> D(nb);
-    std::vector<std::array<int8_t, 5>> pick(nb);   // k >= 2: left share of the split (0: keep whole)
-    for (size_t x = nb; x-- > 0;) {                  // children have larger ids (pre-order)
-        const BNode& c = N[x];
+    // The collapse's dynamic program at node x (see build_wide_sah), run as soon
+    // as both children are built, so it shares the build's threads.
+    std::vector<std::array<double, 5>> D;
+    std::vector<std::array<int8_t, 5>> pick;   // k >= 2: left share of the split (0: keep whole)
+    void collapse_cost(int x) {
+        const BNode& c = nodes[x];
         if (c.left < 0) {
             for (int k = 1; k <= 4; ++k) D[x][k] = 0.0;
-            continue;
+            return;
         }
         auto forest = [&](int k, int8_t& a_best) {
             double best = __builtin_inf();
@@ -337,6 +286,66 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
             }
         }
     }
+};
+
+}  // namespace
+
+// Leaves: the LBVH sorted positions `pos` (all of them, or a subset such as the
+// emissive triangles); leaf_box[6 * p] / leaf_emit[p] by position p.  Writes 32
+// floats per 4-wide node in the inner4 layout of device_api.hpp (breadth-first,
+// root first; child links: id_base + a node's index, or leaf_base + position
+// for a leaf, with the emitter flag in bit 30; -1 none) and returns the node
+// count; *stack_need = the most stack entries the ordered 4-wide walk can hold
+// right after a visit (trace.hip inner_visit4; see below).
+int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
+                   int id_base, std::vector<float>& out, int* stack_need, const WideParams& prm) {
+    const int n = (int)pos.size();
+    out.clear();
+    *stack_need = 0;
+    if (n == 0) return 0;
+    Builder B;
+    B.lbox = leaf_box;
+    B.sweep_max = prm.sweep_max;
+    B.idx = pos;
+    int pmax = 0;
+    for (int p : pos) pmax = std::max(pmax, p);
+    B.cen.resize(3 * (size_t)(pmax + 1));
+    for (int p : pos)
+        for (int k = 0; k < 3; ++k) B.cen[3 * p + k] = 0.5f * (leaf_box[6 * p + k] + leaf_box[6 * p + 3 + k]);
+    B.nodes.assign(2 * (size_t)n - 1, BNode{});
+    B.D.assign(B.nodes.size(), {});
+    B.pick.assign(B.nodes.size(), {});
+    // threads: up to 2^spawn concurrent subtrees, bounded by the cores this process may use
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    int spawn = 0;
+    while (spawn < 5 && (2u << spawn) <= hw) ++spawn;
+    const int root = 0;
+    B.build(0, n, root, leaf_emit, spawn);
+    const auto& N = B.nodes;
+    if (N[root].left < 0) {   // a single leaf: one node holding it
+        out.assign(32, 0.0f);
+        for (int j = 0; j < 3; ++j) {
+            out[j] = N[root].box.lo[j];
+            out[3 + j] = N[root].box.hi[j];
+        }
+        const int32_t links[4] = {(leaf_base + N[root].pos) | (int32_t)(N[root].emit << 30), -1, -1, -1};
+        std::memcpy(out.data() + 24, links, sizeof links);
+        *stack_need = 0;
+        return 1;
+    }
+
+    // Collapse to 4-wide nodes by dynamic programming over the binary tree
+    // (the SAH cost of Ylitie et al. 2017's wide-BVH collapse, 1 triangle per
+    // leaf): D[x][k] is the least cost of representing subtree x as a forest
+    // of at most k subtrees.  Every leaf is some node's child exactly once, so
+    // its triangle-test cost (area-weighted) is the same in every collapse and
+    // drops out; a subtree kept whole costs its area (the probability that its
+    // 4-wide node is visited) plus the best 4-way forest of its children.
+    // Greedy opening of the largest child leaves the bottom levels with 2-leaf
+    // nodes; the DP pulls leaves up into their grandparents.  (Builder::collapse_cost
+    // runs it during the build.)
+    const size_t nb = N.size();
+    const auto& pick = B.pick;
     // Stack bound: a visit of node X finds at most A(X) entries on the stack --
     // the deferred siblings of X and of its ancestors, A(X) = sum over the
     // proper ancestors a of (children(a) - 1) -- and leaves at most A(X) +
