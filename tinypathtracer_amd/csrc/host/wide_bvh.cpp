@@ -22,6 +22,7 @@
 #include <array>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -54,15 +55,31 @@ struct Box {
 
 struct BNode {          // binary SAH node
     Box box;
-    int left = -1, right = -1;   // child BNode ids; a leaf has left = -1
-    int pos = -1;                // leaf: the LBVH sorted position of its triangle
-    uint32_t emit = 0;
+    int left, right;   // child BNode ids; a leaf has left = -1
+    int pos;           // leaf: the LBVH sorted position of its triangle (-1: inner)
+    uint32_t emit;
+};
+
+// A build array left uninitialised: the build writes every element it reads,
+// so each page is first touched by the thread that builds its subtree instead
+// of in one serial zero-fill (≈ 3 ms for 131 K leaves).
+template <class T>
+struct Uninit {
+    std::unique_ptr<T[]> p;
+    size_t n = 0;
+    void reset(size_t m) {
+        p.reset(new T[m]);
+        n = m;
+    }
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+    size_t size() const { return n; }
 };
 
 struct Builder {
     const float* lbox;    // 6 per position
     int sweep_max = 32;   // ranges up to this size split by an exact sweep, larger ones binned
-    std::vector<BNode> nodes;
+    Uninit<BNode> nodes;
     std::vector<int> idx;
     std::vector<float> cen;   // 3 per position
 
@@ -227,6 +244,7 @@ struct Builder {
             nd.pos = idx[b];
             nd.box = leaf_box(idx[b]);
             nd.emit = emit[idx[b]] ? 1u : 0u;
+            nd.left = nd.right = -1;
             collapse_cost(id);
             return;
         }
@@ -242,6 +260,7 @@ struct Builder {
         }
         nd.left = l;
         nd.right = r;
+        nd.pos = -1;
         nd.box = nodes[l].box;
         nd.box.grow(nodes[r].box);
         nd.emit = nodes[l].emit | nodes[r].emit;
@@ -251,8 +270,8 @@ struct Builder {
 
     // The collapse's dynamic program at node x (see build_wide_sah), run as soon
     // as both children are built, so it shares the build's threads.
-    std::vector<std::array<double, 5>> D;
-    std::vector<std::array<int8_t, 5>> pick;   // k >= 2: left share of the split (0: keep whole)
+    Uninit<std::array<double, 5>> D;
+    Uninit<std::array<int8_t, 5>> pick;   // k >= 2: left share of the split (0: keep whole)
     void collapse_cost(int x) {
         const BNode& c = nodes[x];
         if (c.left < 0) {
@@ -312,9 +331,9 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
     B.cen.resize(3 * (size_t)(pmax + 1));
     for (int p : pos)
         for (int k = 0; k < 3; ++k) B.cen[3 * p + k] = 0.5f * (leaf_box[6 * p + k] + leaf_box[6 * p + 3 + k]);
-    B.nodes.assign(2 * (size_t)n - 1, BNode{});
-    B.D.assign(B.nodes.size(), {});
-    B.pick.assign(B.nodes.size(), {});
+    B.nodes.reset(2 * (size_t)n - 1);
+    B.D.reset(B.nodes.size());
+    B.pick.reset(B.nodes.size());
     // threads: up to 2^spawn concurrent subtrees, bounded by the cores this process may use
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     int spawn = 0;
