@@ -64,7 +64,15 @@ typedef struct {
     int32_t mtl;
 } tpt_interval;
 
-/* Host-side scene, the content of DeviceScene (include/mesh.cuh:80-96). */
+/* The content of DeviceScene (include/mesh.cuh:80-96).  Every array pointer
+ * may be host memory or device memory (detected per pointer, as tpt_render
+ * does for its outputs), so the reference's doTrace can pass its
+ * thrust::device_vector buffers as they are -- the `trace` kernel's own
+ * arguments (path_tracer.cu:297-299): raw_pointer_cast(d_scene.indices.data())
+ * etc.  Vec3 arrays are 3 floats per vertex, Mat4 16 floats column-major,
+ * Material is tpt_material byte for byte, MtlInterval is tpt_interval.
+ * The scene keeps its own copy: the caller's buffers are only read during
+ * tpt_scene_create. */
 typedef struct {
     const uint32_t* indices;      uint32_t n_faces;      /* 3*n_faces global vertex ids */
     const float* vertices;        const float* normals;  uint32_t n_vertices; /* xyz, object space */
@@ -72,7 +80,15 @@ typedef struct {
     const float* vert_trans;      const float* normal_trans; /* 16 floats/object, column-major */
     const tpt_material* materials; uint32_t n_materials;   /* empty -> Material() default */
     const tpt_light* lights;      uint32_t n_lights;
+    uint32_t flags;               /* TPT_DESC_*; 0 for a zero-initialised desc */
 } tpt_scene_desc;
+
+/* desc->lights points at the reference's own DeltaLight array (delta_light.h:
+ * 96-130: DeltaLightType, then the PointLight / DirectionalLight / SpotLight
+ * union; 52 B, the offsets of tpt_light except that a directional light keeps
+ * its direction where tpt_light has pos).  The library repacks it; the
+ * union's unused bytes are never read. */
+#define TPT_DESC_DELTALIGHT_LAYOUT 0x1
 
 /* Camera (include/camera.h): c2w = m_transform->localToWorld(). */
 typedef struct {
@@ -163,6 +179,12 @@ tpt_status tpt_scene_create(const tpt_scene_desc* desc, int device, tpt_scene** 
 /* World transform + LBVH build on the device (path_tracer.cu:536-542,
  * bvh.cu:304-331) and the packed traversal layout. */
 tpt_status tpt_scene_build(tpt_scene* scene);
+/* Host threads of the traversal-tree build inside tpt_scene_build (the SAH
+ * 4-wide tree): < 0 = auto (the cores this process may
+ * use: its affinity mask capped by the cgroup CPU quota), 0 or 1 = serial.
+ * Every setting builds the same tree.  Processes sharing a host (one per GPU)
+ * pass their share of the cores. */
+tpt_status tpt_scene_set_build_threads(tpt_scene* scene, int32_t threads);
 void tpt_scene_destroy(tpt_scene* scene);
 
 /* Equirect environment, RGBA8, row 0 = bottom (FreeImage order), already in
@@ -234,9 +256,9 @@ tpt_status tpt_debug_hot_kat(int device, int32_t op, uint32_t n, const float* in
  * leaf boxes (6 floats each, by LBVH sorted position) and emitter flags.  Writes
  * at most `cap` nodes of 32 floats (inner4 layout, device_api.hpp) and the
  * most stack entries its ordered walk can hold; returns the node count (> cap:
- * not written), or -1. */
+ * not written), or -1.  threads as in tpt_scene_set_build_threads. */
 int32_t tpt_wide_tree_build(int32_t n, const float* leaf_box, const uint32_t* leaf_emit, float* nodes,
-                            int32_t cap, int32_t* stack_need);
+                            int32_t cap, int32_t* stack_need, int32_t threads);
 
 /* ---- host-side glTF loader (mesh.cu:80-397 semantics) -------------------- */
 typedef struct tpt_gltf tpt_gltf;

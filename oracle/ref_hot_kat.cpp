@@ -18,6 +18,16 @@
 //   A dist r g b               -> "A r g b"                     CalcDistAttenuation
 //   U r g b                    -> "U x y z" (decimal bytes)     Spectrum::toUChar
 //   M                          -> "M" + 15 floats               Material() defaults
+//   S                          -> "S" + decimal byte sizes and offsets of the
+//                                 structs the C-ABI takes as they are (tpt.h):
+//                                 sizeof(DeltaLight), then the offsets within
+//                                 DeltaLight of type, pl.color, pl.intensity,
+//                                 pl.pos, dl.color, dl.intensity, dl.direction,
+//                                 sl.color, sl.intensity, sl.pos, sl.direction,
+//                                 sl.cosOuterAngle, sl.invCosConeDifference;
+//                                 sizeof(Material), offsets of baseColor,
+//                                 emissionFactor, eta, metallic, clearcoatGloss;
+//                                 sizeof(Vec3), sizeof(Spectrum)
 #include <cfloat>
 #include <hip/hip_runtime.h>
 
@@ -119,6 +129,22 @@ int main() {
             pf(m.roughness); pf(m.specularTint); pf(m.anisotropic); pf(m.sheen); pf(m.sheenTint);
             pf(m.clearcoat); pf(m.clearcoatGloss);
             std::printf("\n");
+        } else if (op == "S" && n == 0) {
+            DeltaLight d;
+            Material m;
+            const char* b = (const char*)&d;
+            auto off = [&](const void* p) { return (long)((const char*)p - b); };
+            const char* mb = (const char*)&m;
+            auto moff = [&](const void* p) { return (long)((const char*)p - mb); };
+            std::printf("S %zu %ld %ld %ld %ld %ld %ld %ld %ld %ld %ld %ld %ld %ld", sizeof(DeltaLight), off(&d.type),
+                        off(&d.light.pl.color), off(&d.light.pl.intensity), off(&d.light.pl.pos),
+                        off(&d.light.dl.color), off(&d.light.dl.intensity), off(&d.light.dl.direction),
+                        off(&d.light.sl.color), off(&d.light.sl.intensity), off(&d.light.sl.pos),
+                        off(&d.light.sl.direction), off(&d.light.sl.cosOuterAngle),
+                        off(&d.light.sl.invCosConeDifference));
+            std::printf(" %zu %ld %ld %ld %ld %ld %zu %zu\n", sizeof(Material), moff(&m.baseColor),
+                        moff(&m.emissionFactor), moff(&m.eta), moff(&m.metallic), moff(&m.clearcoatGloss),
+                        sizeof(Vec3), sizeof(Spectrum));
         } else {
             std::printf("E\n");
         }

@@ -220,10 +220,12 @@ def make_ref_hot_kat():
             keys.append(op)
     reqs.append("M")
     keys.append("M")
+    reqs.append("S")
+    keys.append("S")
     res = subprocess.run([exe], input="\n".join(reqs) + "\n", capture_output=True, text=True, check=True)
     lines = res.stdout.strip().split("\n")
     assert len(lines) == len(reqs)
-    out = {k: [] for k in ("B", "X", "L", "A", "U", "M")}
+    out = {k: [] for k in ("B", "X", "L", "A", "U", "M", "S")}
     for op, req, line in zip(keys, reqs, lines):
         parts = line.split()
         assert parts[0] == op, (req, line)

@@ -174,3 +174,31 @@ def test_kernel_light_and_bytes_match_reference(kat, gpu_available):
     rows = _rows(kat, "U")
     got = T.hot_kat(3, np.stack([r for r, _ in rows]))
     assert np.array_equal(got.astype(int), np.array([[int(v) for v in o] for _, o in rows]))
+
+
+def test_abi_structs_match_reference_layouts(kat):
+    """The C-ABI takes the reference's device arrays as they are (tpt.h
+    tpt_scene_desc): Material is tpt_material byte for byte, and DeltaLight
+    (delta_light.h:96-130) has tpt_light's offsets except that a directional
+    light's direction shares pos's bytes (TPT_DESC_DELTALIGHT_LAYOUT).  The
+    sizes and offsets come from the reference's own headers compiled here
+    (oracle/_ref/ref_hot_kat op S)."""
+    from tinypathtracer_amd import _lib
+    out = [int(x) for x in kat["S"][0]["out"]]
+    dl_size, o_type, pl_col, pl_int, pl_pos, dl_col, dl_int, dl_dir, sl_col, sl_int, sl_pos, sl_dir, sl_cos, sl_inv = \
+        out[:14]
+    m_size, m_base, m_emit, m_eta, m_metal, m_gloss, vec3, spec = out[14:]
+    L = _lib.Light
+    assert dl_size == C.sizeof(L) == 52
+    assert o_type == L.type.offset
+    for col, inten in ((pl_col, pl_int), (dl_col, dl_int), (sl_col, sl_int)):
+        assert col == L.color.offset and inten == L.intensity.offset
+    assert pl_pos == sl_pos == L.pos.offset
+    assert dl_dir == L.pos.offset                 # the union remap the library applies
+    assert sl_dir == L.direction.offset
+    assert sl_cos == L.cos_outer.offset and sl_inv == L.inv_cos_cone_diff.offset
+    M = _lib.Material
+    assert m_size == C.sizeof(M) == 60
+    assert m_base == M.base_color.offset and m_emit == M.emission_factor.offset
+    assert m_eta == M.eta.offset and m_metal == M.metallic.offset and m_gloss == M.clearcoat_gloss.offset
+    assert vec3 == 12 and spec == 12              # Vec3 / Spectrum: 3 floats, no padding

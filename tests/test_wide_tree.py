@@ -36,13 +36,14 @@ def _leaves(name):
     return n, box, emit
 
 
-def _build(n, box, emit):
+def _build(n, box, emit, threads=-1):
     lib = T.lib()
     lv = C.c_int32(0)
-    cnt = lib.tpt_wide_tree_build(n, box.ctypes.data, emit.ctypes.data, None, 0, C.byref(lv))
+    cnt = lib.tpt_wide_tree_build(n, box.ctypes.data, emit.ctypes.data, None, 0, C.byref(lv), threads)
     assert cnt > 0
     out = np.zeros((cnt, 32), np.float32)
-    assert lib.tpt_wide_tree_build(n, box.ctypes.data, emit.ctypes.data, out.ctypes.data, cnt, C.byref(lv)) == cnt
+    assert lib.tpt_wide_tree_build(n, box.ctypes.data, emit.ctypes.data, out.ctypes.data, cnt, C.byref(lv),
+                                   threads) == cnt
     return out, lv.value
 
 
@@ -138,3 +139,31 @@ def test_wide_tree_reaches_every_passing_leaf():
                 else:
                     stack.append(cid)
         assert got == want
+
+
+def _random_leaves(n, seed):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-50.0, 50.0, (n, 3)).astype(np.float32)
+    e = rng.uniform(0.01, 2.0, (n, 3)).astype(np.float32)
+    box = np.concatenate([c - e, c + e], axis=1).astype(np.float32)
+    emit = (rng.random(n) < 0.01).astype(np.uint32)
+    return box, emit
+
+
+@pytest.mark.parametrize("case", ["c5", "random"])
+def test_threaded_build_equals_serial_build(case):
+    """The threaded SAH build (subtrees of >= 4096 leaves on their own threads,
+    host/wide_bvh.cpp) writes the same node array as the serial build, byte for
+    byte, for every thread count -- pre-order ids are fixed before a subtree is
+    built, so only the schedule differs."""
+    if case == "c5":
+        n, box, emit = _leaves("c5")
+    else:
+        n = 40000
+        box, emit = _random_leaves(n, 11)
+    serial, need = _build(n, box, emit, threads=0)
+    assert n > 8192   # large enough that the threaded path spawns
+    for threads in (1, 2, 3, 8, 32, -1):
+        got, need2 = _build(n, box, emit, threads=threads)
+        assert need2 == need
+        assert got.tobytes() == serial.tobytes(), threads

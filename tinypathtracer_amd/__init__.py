@@ -124,17 +124,79 @@ class Scene:
     def copySceneToDevice(self, device: int = 0) -> "DeviceScene":
         return DeviceScene(self, device)
 
+    def device_buffers(self, device: int = 0) -> dict:
+        """The reference's DeviceScene (mesh.cuh:80-96) as torch tensors in HBM of
+        `device`, element types and layouts as the reference's thrust
+        device_vectors hold them: indices u32, Vec3 vertices/normals, Material
+        (15 floats), MtlInterval, column-major Mat4, and DeltaLight
+        (delta_light.h:96-130, 52 B: the type, then the light union -- a
+        directional light's direction where the others keep pos; bytes a light
+        type does not own are NaN here, so a reader of them would show).  These
+        are the `trace` kernel's own arguments (path_tracer.cu:297-299);
+        DeviceScene(scene, device, buffers=...) hands them to tpt_scene_create
+        as device pointers."""
+        import torch
+        dev = torch.device("cuda", device)
+        lights = np.full((max(len(self.lights), 1), 13), np.nan, np.float32)
+        for i, L in enumerate(self.lights):
+            row = lights[i]
+            row[0:1].view(np.int32)[0] = L.type
+            row[1:4] = L.color[:]
+            row[4] = L.intensity
+            if L.type == 1:    # DirectionalLight{color, intensity, direction}
+                row[5:8] = L.direction[:]
+            else:              # PointLight{color, intensity, pos}; SpotLight{..., pos, direction, cos, invDiff}
+                row[5:8] = L.pos[:]
+                if L.type == 2:
+                    row[8:11] = L.direction[:]
+                    row[11] = L.cos_outer
+                    row[12] = L.inv_cos_cone_diff
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev) if len(a) else \
+            torch.empty(0, dtype=dt, device=dev)
+        bufs = {
+            "indices": t(self.indices.astype(np.uint32).view(np.int32), torch.int32),
+            "vertices": t(self.vertices.astype(np.float32), torch.float32),
+            "normals": t(self.normals.astype(np.float32), torch.float32),
+            "materials": t(self.materials.astype(np.float32), torch.float32),
+            "materialsLUT": t(self.lut.astype(np.int32), torch.int32),
+            "vertTrans": t(self.vert_trans.astype(np.float32), torch.float32),
+            "normalTrans": t(self.normal_trans.astype(np.float32), torch.float32),
+            "lights": t(lights[:len(self.lights)], torch.float32),
+        }
+        torch.cuda.synchronize(dev)
+        return bufs
+
 
 class DeviceScene:
     """DeviceScene (mesh.cuh:80-96): scene buffers resident in HBM of `device`."""
 
-    def __init__(self, scene: Scene, device: int = 0):
+    def __init__(self, scene: Scene, device: int = 0, buffers: dict | None = None):
+        """buffers: Scene.device_buffers() -- device arrays in the reference's
+        layouts, passed to tpt_scene_create as device pointers (the reference's
+        doTrace hands over its DeviceScene this way)."""
         self.scene = scene
         self.device = device
         self.handle = C.c_void_p()
-        d = scene.desc()
+        if buffers is None:
+            d = scene.desc()
+        else:
+            b = buffers
+            dp = lambda k, ty: C.cast(C.c_void_p(b[k].data_ptr() if b[k].numel() else 0), C.POINTER(ty))
+            d = _lib.SceneDesc(
+                dp("indices", C.c_uint32), b["indices"].numel() // 3,
+                dp("vertices", C.c_float), dp("normals", C.c_float), b["vertices"].numel() // 3,
+                dp("materialsLUT", _lib.Interval), b["materialsLUT"].numel() // 2,
+                dp("vertTrans", C.c_float), dp("normalTrans", C.c_float),
+                dp("materials", _lib.Material), b["materials"].numel() // 15,
+                dp("lights", _lib.Light), b["lights"].numel() // 13, _lib.DESC_DELTALIGHT_LAYOUT)
         check(lib().tpt_scene_create(C.byref(d), device, C.byref(self.handle)))
         self.built = False
+
+    def set_build_threads(self, threads: int):
+        """Host threads of the traversal-tree build (tpt_scene_set_build_threads):
+        < 0 the usable cores, 0/1 serial; the same tree either way."""
+        check(lib().tpt_scene_set_build_threads(self.handle, int(threads)))
+        return self
 
     def build(self):
         """World transform + LBVH (path_tracer.cu:536-542) on the device."""

@@ -19,6 +19,7 @@ FLAG_REF_ORDER = 0x2
 FLAG_ACCUMULATE = 0x4
 FLAG_ENV_IS = 0x8
 FLAG_APPROX_CULL = 0x10
+DESC_DELTALIGHT_LAYOUT = 0x1
 
 
 class Material(C.Structure):
@@ -45,7 +46,7 @@ class SceneDesc(C.Structure):
                 ("n_vertices", C.c_uint32), ("lut", C.POINTER(Interval)), ("n_objects", C.c_uint32),
                 ("vert_trans", C.POINTER(C.c_float)), ("normal_trans", C.POINTER(C.c_float)),
                 ("materials", C.POINTER(Material)), ("n_materials", C.c_uint32),
-                ("lights", C.POINTER(Light)), ("n_lights", C.c_uint32)]
+                ("lights", C.POINTER(Light)), ("n_lights", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class Camera(C.Structure):
@@ -79,6 +80,7 @@ SIGNATURES = [
     ("tpt_device_count", C.c_int, []),
     ("tpt_scene_create", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     ("tpt_scene_build", C.c_int, [C.c_void_p]),
+    ("tpt_scene_set_build_threads", C.c_int, [C.c_void_p, C.c_int32]),
     ("tpt_scene_destroy", None, [C.c_void_p]),
     ("tpt_env_create", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int, C.POINTER(C.c_void_p)]),
     ("tpt_env_destroy", None, [C.c_void_p]),
@@ -98,7 +100,7 @@ SIGNATURES = [
                                        C.c_void_p, C.c_void_p]),
     ("tpt_debug_hot_kat", C.c_int, [C.c_int, C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("tpt_wide_tree_build", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
-                                        C.POINTER(C.c_int32)]),
+                                        C.POINTER(C.c_int32), C.c_int32]),
     ("tpt_gltf_load", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
     ("tpt_gltf_desc", C.c_int, [C.c_void_p, C.POINTER(SceneDesc), C.POINTER(Camera)]),
     ("tpt_gltf_missing_material", C.c_int, [C.c_void_p]),

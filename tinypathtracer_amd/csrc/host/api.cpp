@@ -92,6 +92,21 @@ bool is_device_ptr(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+// A desc array in device memory (the reference's DeviceScene buffers) read back
+// to the host, or the host array itself.  Returns the host view (null on a
+// failed copy, with *err set).
+template <typename T>
+const T* host_view(const T* p, size_t n, std::vector<T>& tmp, hipError_t* err) {
+    if (!p || n == 0 || !is_device_ptr(p)) return p;
+    tmp.resize(n);
+    const hipError_t e = hipMemcpy(tmp.data(), p, n * sizeof(T), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        *err = e;
+        return nullptr;
+    }
+    return tmp.data();
+}
+
 std::vector<uint32_t>& host_jumps() {
     static std::vector<uint32_t> j;
     if (j.empty()) {
@@ -178,6 +193,7 @@ struct tpt_scene {
     DevBuf<float4> sliver_groups, sliver_list;
     float cull_eps = 0.0f;                  // absolute position slack of the t-culls
     uint32_t tree_depth = 0;
+    int32_t build_threads = -1;             // SAH tree build threads (tpt_scene_set_build_threads)
     // inputs
     DevBuf<uint32_t> indices;
     DevBuf<float> vertices, normals, vert_trans, normal_trans;
@@ -268,23 +284,46 @@ int tpt_device_count(void) {
     return n;
 }
 
-tpt_status tpt_scene_create(const tpt_scene_desc* d, int device, tpt_scene** out) {
-    if (!d || !out) return fail(TPT_ERR_INVALID_ARG, "null argument");
+tpt_status tpt_scene_create(const tpt_scene_desc* d_in, int device, tpt_scene** out) {
+    if (!d_in || !out) return fail(TPT_ERR_INVALID_ARG, "null argument");
     *out = nullptr;
-    if (d->n_faces == 0 || !d->indices || !d->vertices || !d->normals || d->n_vertices == 0)
+    if (d_in->n_faces == 0 || !d_in->indices || !d_in->vertices || !d_in->normals || d_in->n_vertices == 0)
         return fail(TPT_ERR_INVALID_ARG, "scene needs faces, vertices and normals");
-    if (d->n_objects == 0 || !d->lut || !d->vert_trans || !d->normal_trans)
+    if (d_in->n_objects == 0 || !d_in->lut || !d_in->vert_trans || !d_in->normal_trans)
         return fail(TPT_ERR_INVALID_ARG, "scene needs at least one object (LUT + transforms)");
-    if (d->n_lights > (uint32_t)tpt::kMaxLights) return fail(TPT_ERR_INVALID_ARG, "too many delta lights (max 16)");
-    if (d->n_faces > (1u << 30)) return fail(TPT_ERR_INVALID_ARG, "too many faces");
-    for (uint64_t i = 0; i < 3ull * d->n_faces; ++i)
-        if (d->indices[i] >= d->n_vertices) return fail(TPT_ERR_INVALID_ARG, "vertex index out of range");
-    if (d->lut[0].begin != 0) return fail(TPT_ERR_INVALID_ARG, "first object must begin at face 0");
+    if (d_in->n_lights > (uint32_t)tpt::kMaxLights) return fail(TPT_ERR_INVALID_ARG, "too many delta lights (max 16)");
+    if (d_in->n_lights > 0 && !d_in->lights) return fail(TPT_ERR_INVALID_ARG, "null light array");
+    if (d_in->n_faces > (1u << 30)) return fail(TPT_ERR_INVALID_ARG, "too many faces");
+    if (d_in->flags & ~(uint32_t)TPT_DESC_DELTALIGHT_LAYOUT) return fail(TPT_ERR_INVALID_ARG, "unknown desc flags");
     int ndev = tpt_device_count();
     if (ndev <= 0) return fail(TPT_ERR_NO_DEVICE, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(TPT_ERR_INVALID_ARG, "bad device index");
 
     DeviceGuard g(device);
+    // Arrays may live in device memory (DeviceScene's thrust buffers, the
+    // `trace` kernel's arguments): the small ones and the indices (validated
+    // here) are read back; vertices and normals are copied device to device.
+    tpt_scene_desc dh = *d_in;
+    const tpt_scene_desc* d = &dh;
+    std::vector<uint32_t> t_idx;
+    std::vector<tpt_interval> t_lut;
+    std::vector<float> t_vt, t_nt;
+    std::vector<tpt_material> t_mtl;
+    std::vector<tpt_light> t_lights;
+    hipError_t herr = hipSuccess;
+    dh.indices = host_view(d_in->indices, 3 * (size_t)d_in->n_faces, t_idx, &herr);
+    dh.lut = host_view(d_in->lut, d_in->n_objects, t_lut, &herr);
+    dh.vert_trans = host_view(d_in->vert_trans, 16 * (size_t)d_in->n_objects, t_vt, &herr);
+    dh.normal_trans = host_view(d_in->normal_trans, 16 * (size_t)d_in->n_objects, t_nt, &herr);
+    dh.materials = host_view(d_in->materials, d_in->n_materials, t_mtl, &herr);
+    dh.lights = host_view(d_in->lights, d_in->n_lights, t_lights, &herr);
+    if (herr != hipSuccess) return fail(TPT_ERR_HIP, std::string("scene desc readback: ") + hipGetErrorString(herr));
+    const bool verts_dev = is_device_ptr(d_in->vertices), norms_dev = is_device_ptr(d_in->normals);
+
+    for (uint64_t i = 0; i < 3ull * d->n_faces; ++i)
+        if (d->indices[i] >= d->n_vertices) return fail(TPT_ERR_INVALID_ARG, "vertex index out of range");
+    if (d->lut[0].begin != 0) return fail(TPT_ERR_INVALID_ARG, "first object must begin at face 0");
+
     tpt_scene* s = new (std::nothrow) tpt_scene();
     if (!s) return fail(TPT_ERR_OOM, "host allocation failed");
     s->device = device;
@@ -311,23 +350,53 @@ tpt_status tpt_scene_create(const tpt_scene_desc* d, int device, tpt_scene** out
         mtl[2 * i] = make_float4(m.base_color[0], m.base_color[1], m.base_color[2], m.emission_factor);
         mtl[2 * i + 1] = make_float4(m.eta, m.metallic, 0.0f, 0.0f);
     }
+    const bool union_layout = (d->flags & TPT_DESC_DELTALIGHT_LAYOUT) != 0;
     std::vector<tpt::DevLight> lights(d->n_lights);
     for (uint32_t i = 0; i < d->n_lights; ++i) {
         const tpt_light& L = d->lights[i];
+        if (L.type < 0 || L.type > 2) return cleanup(fail(TPT_ERR_INVALID_ARG, "unknown delta light type"));
         tpt::DevLight& o = lights[i];
         o.type = L.type;
         std::memcpy(o.color, L.color, sizeof o.color);
         o.intensity = L.intensity;
-        std::memcpy(o.pos, L.pos, sizeof o.pos);
-        std::memcpy(o.dir, L.direction, sizeof o.dir);
-        o.cos_outer = L.cos_outer;
-        o.inv_cos_cone_diff = L.inv_cos_cone_diff;
+        if (union_layout) {
+            // DeltaLight (delta_light.h:96-130): the union's members share their
+            // first bytes -- color, intensity, then PointLight::pos /
+            // DirectionalLight::direction / SpotLight::pos; only a spot light has
+            // the direction and cone fields behind them.  Bytes a light type does
+            // not own are not read.
+            std::memset(o.pos, 0, sizeof o.pos);
+            std::memset(o.dir, 0, sizeof o.dir);
+            o.cos_outer = 0.0f;
+            o.inv_cos_cone_diff = 0.0f;
+            if (L.type == 1) {
+                std::memcpy(o.dir, L.pos, sizeof o.dir);
+            } else {
+                std::memcpy(o.pos, L.pos, sizeof o.pos);
+                if (L.type == 2) {
+                    std::memcpy(o.dir, L.direction, sizeof o.dir);
+                    o.cos_outer = L.cos_outer;
+                    o.inv_cos_cone_diff = L.inv_cos_cone_diff;
+                }
+            }
+        } else {
+            std::memcpy(o.pos, L.pos, sizeof o.pos);
+            std::memcpy(o.dir, L.direction, sizeof o.dir);
+            o.cos_outer = L.cos_outer;
+            o.inv_cos_cone_diff = L.inv_cos_cone_diff;
+        }
     }
     const auto& jumps = host_jumps();
     hipStream_t st = s->stream;
+    auto copy_in = [&](DevBuf<float>& dst, const float* src, size_t count, bool dev) {
+        if (!dev) return dst.upload(src, count, st);
+        hipError_t e2 = dst.alloc(count);
+        if (e2 == hipSuccess) e2 = hipMemcpyAsync(dst.p, src, count * sizeof(float), hipMemcpyDeviceToDevice, st);
+        return e2;
+    };
     e = s->indices.upload(d->indices, 3 * (size_t)d->n_faces, st);
-    if (e == hipSuccess) e = s->vertices.upload(d->vertices, 3 * (size_t)d->n_vertices, st);
-    if (e == hipSuccess) e = s->normals.upload(d->normals, 3 * (size_t)d->n_vertices, st);
+    if (e == hipSuccess) e = copy_in(s->vertices, d_in->vertices, 3 * (size_t)d->n_vertices, verts_dev);
+    if (e == hipSuccess) e = copy_in(s->normals, d_in->normals, 3 * (size_t)d->n_vertices, norms_dev);
     if (e == hipSuccess) e = s->lut.upload(lut.data(), lut.size(), st);
     if (e == hipSuccess) e = s->vert_trans.upload(d->vert_trans, 16 * (size_t)d->n_objects, st);
     if (e == hipSuccess) e = s->normal_trans.upload(d->normal_trans, 16 * (size_t)d->n_objects, st);
@@ -339,6 +408,12 @@ tpt_status tpt_scene_create(const tpt_scene_desc* d, int device, tpt_scene** out
         return cleanup(fail(e == hipErrorOutOfMemory ? TPT_ERR_OOM : TPT_ERR_HIP,
                             std::string("scene upload: ") + hipGetErrorString(e)));
     *out = s;
+    return TPT_OK;
+}
+
+tpt_status tpt_scene_set_build_threads(tpt_scene* s, int32_t threads) {
+    if (!s) return fail(TPT_ERR_INVALID_ARG, "null scene");
+    s->build_threads = threads;
     return TPT_OK;
 }
 
@@ -535,6 +610,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
             s->n_sliver_groups = (int32_t)grp.size();
         }
         tpt::WideParams prm;
+        prm.threads = s->build_threads;
 #ifdef TPT_WIDE_SWEEP
         prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
 #endif
@@ -550,7 +626,14 @@ tpt_status tpt_scene_build(tpt_scene* s) {
             for (size_t p = 0; p < n; ++p) all[p] = (int)p;
             std::vector<float> w4;
             int need = 0;
-            const int n4 = tpt::build_wide_sah(all, lbox.data(), lemit.data(), leaf_base, 0, w4, &need, prm);
+            int n4 = -1;
+            try {
+                n4 = tpt::build_wide_sah(all, lbox.data(), lemit.data(), leaf_base, 0, w4, &need, prm);
+            } catch (const std::bad_alloc&) {
+                return fail(TPT_ERR_OOM, "traversal tree build: host allocation failed");
+            } catch (const std::exception& ex) {
+                return fail(TPT_ERR_HIP, std::string("traversal tree build: ") + ex.what());
+            }
             if (n4 > 0 && (size_t)n4 <= n - 1 && need <= 150) {
                 HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, w4.data(), w4.size() * sizeof(float),
                                            hipMemcpyHostToDevice, s->stream));
@@ -569,7 +652,14 @@ tpt_status tpt_scene_build(tpt_scene* s) {
         if (!em.empty()) {
             std::vector<float> e4;
             int eneed = 0;
-            const int ne4 = tpt::build_wide_sah(em, lbox.data(), lemit.data(), leaf_base, s->n4, e4, &eneed, prm);
+            int ne4 = -1;
+            try {
+                ne4 = tpt::build_wide_sah(em, lbox.data(), lemit.data(), leaf_base, s->n4, e4, &eneed, prm);
+            } catch (const std::bad_alloc&) {
+                return fail(TPT_ERR_OOM, "emitter tree build: host allocation failed");
+            } catch (const std::exception& ex) {
+                return fail(TPT_ERR_HIP, std::string("emitter tree build: ") + ex.what());
+            }
             if (ne4 > 0 && (size_t)(s->n4 + ne4) <= n - 1 && eneed <= 150) {
                 HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p + 8 * (size_t)s->n4, e4.data(), e4.size() * sizeof(float),
                                            hipMemcpyHostToDevice, s->stream));
@@ -734,8 +824,6 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     const size_t nf = (size_t)n_frames;
     const int bh = band_height_of(H, band_rows, band_count, p->band_index);
     const std::vector<uint64_t> fseeds(seeds, seeds + nf);
-    // the trace grid's y extent is (band row blocks) x frames
-    if ((size_t)((bh + 7) / 8) * nf > 65535) return fail(TPT_ERR_INVALID_ARG, "frame batch too large for one launch");
 
     const bool resume = (p->flags & TPT_FLAG_ACCUMULATE) && s->acc_valid && s->acc_w == W && s->acc_h == H &&
                         s->acc_rows == band_rows && s->acc_count == band_count && s->acc_index == p->band_index &&
@@ -788,6 +876,13 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // the threshold scales down with them (C3 1080p 4096 spp: 24 -> 5.88,
     // 8 -> 6.44, 2..12 within 6.2-6.6 Grays/s; C2 single-lane: 16-24 best).
     const bool pair_kernel = a.pair && s->n_lights > 0 && (s->n_materials + 1) < 0x7fff;
+    // the trace grid's y extent is (band row blocks) x frames: 8-row workgroups in
+    // pair mode, 16 otherwise (launch_trace)
+    {
+        const int wg_rows = (pair_kernel && !a.env_is && !(p->flags & TPT_FLAG_REF_ORDER)) ? 8 : 16;
+        if ((size_t)((bh + wg_rows - 1) / wg_rows) * nf > 65535)
+            return fail(TPT_ERR_INVALID_ARG, "frame batch too large for one launch");
+    }
     // A launch with fewer pixels than about twice the chip's resident lanes
     // (256 CUs x 4 SIMDs x 5 waves x 64 = 327,680: strong-scaled frames, small
     // images) is bound by its heaviest waves' chains, not by throughput: batch
@@ -1179,6 +1274,7 @@ tpt_status tpt_gltf_desc(const tpt_gltf* g, tpt_scene_desc* d, tpt_camera* cam) 
     d->n_materials = (uint32_t)h.materials.size();
     d->lights = h.lights.empty() ? nullptr : h.lights.data();
     d->n_lights = (uint32_t)h.lights.size();
+    d->flags = 0;
     if (cam) *cam = h.camera;
     return TPT_OK;
 }

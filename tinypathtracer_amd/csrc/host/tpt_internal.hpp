@@ -50,7 +50,9 @@ void load_image(const std::string& path, std::vector<uint8_t>& rgba, int& w, int
 // (wide_bvh.cpp): 32 floats per node in the inner4 layout; returns the node count.
 struct WideParams {
     int sweep_max = 32;    // SAH ranges up to this size use an exact sweep, larger ones 32 bins
+    int threads = -1;      // build threads: < 0 the usable cores (affinity, cgroup quota); 0, 1 serial
 };
+int usable_cores();
 int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
                    int id_base, std::vector<float>& out, int* stack_need, const WideParams& prm);
 

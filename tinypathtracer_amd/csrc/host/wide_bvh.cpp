@@ -21,10 +21,16 @@
 #include <algorithm>
 #include <array>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
+#include <system_error>
 #include <thread>
 #include <vector>
+
+#include <sched.h>
 
 #include "tpt_internal.hpp"
 
@@ -250,11 +256,37 @@ struct Builder {
         }
         const int s = split(b, e);
         const int l = id + 1, r = id + 2 * (s - b);
+        bool serial = true;
         if (spawn > 0 && s - b >= kParMin && e - s >= kParMin) {
-            std::thread t([&, b, s, l] { build(b, s, l, emit, spawn - 1); });
-            build(s, e, r, emit, spawn - 1);
-            t.join();
-        } else {   // (a lopsided split keeps its threads for the larger side)
+            // The left subtree on its own thread.  Exceptions (bad_alloc in the
+            // subtree) are carried back and rethrown after the join; a thread
+            // that cannot be started (std::system_error under a pid or ulimit
+            // cap) leaves the subtree to this thread -- the same tree either way.
+            std::exception_ptr err;
+            std::thread t;
+            try {
+                t = std::thread([&, b, s, l] {
+                    try {
+                        build(b, s, l, emit, spawn - 1);
+                    } catch (...) {
+                        err = std::current_exception();
+                    }
+                });
+                serial = false;
+            } catch (const std::system_error&) {
+            }
+            if (!serial) {
+                try {
+                    build(s, e, r, emit, spawn - 1);
+                } catch (...) {
+                    t.join();
+                    throw;
+                }
+                t.join();
+                if (err) std::rethrow_exception(err);
+            }
+        }
+        if (serial) {   // (a lopsided split keeps its threads for the larger side)
             build(b, s, l, emit, spawn);
             build(s, e, r, emit, spawn);
         }
@@ -309,6 +341,27 @@ struct Builder {
 
 }  // namespace
 
+// Host cores this process may use: its CPU affinity mask, capped by a cgroup v2
+// CPU quota (/sys/fs/cgroup/cpu.max).  std::thread::hardware_concurrency()
+// reports every CPU of the host (256 on the GPU box, whose quota is 16).
+int usable_cores() {
+    int n = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::max(1u, std::thread::hardware_concurrency());
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long per = 0;
+        if (std::fscanf(f, "%31s %lld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0) {
+            const long long quota = std::atoll(q);
+            if (quota > 0) n = std::min<long long>(n, std::max<long long>(1, quota / per));
+        }
+        std::fclose(f);
+    }
+    return std::max(1, n);
+}
+
 // Leaves: the LBVH sorted positions `pos` (all of them, or a subset such as the
 // emissive triangles); leaf_box[6 * p] / leaf_emit[p] by position p.  Writes 32
 // floats per 4-wide node in the inner4 layout of device_api.hpp (breadth-first,
@@ -334,10 +387,11 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
     B.nodes.reset(2 * (size_t)n - 1);
     B.D.reset(B.nodes.size());
     B.pick.reset(B.nodes.size());
-    // threads: up to 2^spawn concurrent subtrees, bounded by the cores this process may use
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    // threads: up to 2^spawn concurrent subtrees, at most prm.threads (< 0: the
+    // cores this process may use; 0 or 1: a serial build -- the same tree)
+    const int hw = prm.threads < 0 ? usable_cores() : prm.threads;
     int spawn = 0;
-    while (spawn < 5 && (2u << spawn) <= hw) ++spawn;
+    while (spawn < 5 && (2 << spawn) <= hw) ++spawn;
     const int root = 0;
     B.build(0, n, root, leaf_emit, spawn);
     const auto& N = B.nodes;
@@ -434,13 +488,20 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
 }  // namespace tpt
 
 extern "C" int32_t tpt_wide_tree_build(int32_t n, const float* leaf_box, const uint32_t* leaf_emit, float* nodes,
-                                       int32_t cap, int32_t* stack_need) {
+                                       int32_t cap, int32_t* stack_need, int32_t threads) {
     if (n < 2 || !leaf_box || !leaf_emit || cap < 0) return -1;
     std::vector<float> out;
     int lv = 0;
-    std::vector<int> pos(n);
-    for (int p = 0; p < n; ++p) pos[p] = p;
-    const int n4 = tpt::build_wide_sah(pos, leaf_box, leaf_emit, n - 1, 0, out, &lv, tpt::WideParams{});
+    int n4 = -1;
+    try {
+        std::vector<int> pos(n);
+        for (int p = 0; p < n; ++p) pos[p] = p;
+        tpt::WideParams prm;
+        prm.threads = threads;
+        n4 = tpt::build_wide_sah(pos, leaf_box, leaf_emit, n - 1, 0, out, &lv, prm);
+    } catch (const std::exception&) {
+        return -1;
+    }
     if (stack_need) *stack_need = lv;
     if (n4 <= cap && nodes) std::memcpy(nodes, out.data(), out.size() * sizeof(float));
     return n4;
