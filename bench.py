@@ -8,14 +8,19 @@ copyToFB, inputs resident in HBM.  A "ray" is one traverseBVH call (primary,
 extension, direct probe, shadow), counted by the kernel.
 
 N GPUs: one process per GPU (torch.distributed.run).  Default (--scaling
-weak): a step is a batch of N frames of the workload above (seeds 42 .. 42+N-1;
-the reference re-seeds every frame, path_tracer.cu:493,513), each frame split
-across all N GPUs in interleaved 16-row bands, so every GPU renders the pixel
-mix of one whole frame in one launch; one all-to-all (RCCL over xGMI) leaves
-frame f on rank f inside the timed region.  --scaling strong: one frame split
-across the N GPUs, one gather to rank 0 (bounded by the heaviest pixels'
-serial sample chains).  value = rays of all frames /
-max-over-ranks step time.
+strong, the split north_star names): a step is ONE frame of the workload
+above, dealt to the N GPUs in interleaved 16-row pixel bands, and one gather
+of the framebuffer bands to rank 0 (RCCL over xGMI) inside the timed region.
+value = the frame's rays / max-over-ranks step time.  The same run then also
+times weak scaling (key "weak"; --weak-extra 0 skips it): a step is a batch of
+N frames (seeds 42 .. 42+N-1; the reference re-seeds every frame,
+path_tracer.cu:493,513), each frame banded across all N GPUs, one all-to-all
+leaving frame f on rank f.  --scaling weak makes that the headline instead.
+
+--emulate-ranks N (one GPU): renders every rank's share of an N-way split in
+turn and reports the slowest rank's step time (the multi-GPU step is the max
+over ranks) and the rays of all N shares; --emulate-rank0-only times rank 0's
+share alone.
 
 A step is the reference's doTrace (path_tracer.cu:491-554) in full: the
 world transform and BVH build (:536-542, transform + LBVH + the 4-wide
@@ -70,11 +75,18 @@ def parse():
                     help="gloo: rehearse the N-rank path on one GPU (all ranks on device 0, gather via host)")
     ap.add_argument("--verify-gather", action="store_true",
                     help="rank 0 re-renders the whole frame alone and checks the gathered frame bit for bit")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: N frames per step, each banded across the N ranks (all-to-all); "
-                         "strong: one frame banded across the N ranks (gather)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong: one frame banded across the N ranks (gather); "
+                         "weak: N frames per step, each banded across the N ranks (all-to-all)")
+    ap.add_argument("--weak-extra", type=int, default=1,
+                    help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
     ap.add_argument("--emulate-ranks", type=int, default=0,
-                    help="1-GPU rehearsal of an N-rank run: render only rank 0's bands of an N-way split")
+                    help="1-GPU rehearsal of an N-rank run: every rank's bands of an N-way split in turn, "
+                         "the step = the slowest rank's")
+    ap.add_argument("--emulate-rank0-only", action="store_true", help="with --emulate-ranks: rank 0's share only")
+    ap.add_argument("--build-threads", type=int, default=-2,
+                    help="host threads of the traversal-tree build (tpt_scene_set_build_threads); "
+                         "-2: this process's share of the usable cores (cores / local ranks)")
     ap.add_argument("--env", choices=["sky", "none"], default=None, help="procedural equirect env on miss")
     ap.add_argument("--env-is", action="store_true",
                     help="opt-in env next-event estimation with importance sampling (A15; changes the image)")
@@ -300,6 +312,10 @@ def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_lau
             "avg_launch_ms": round(avg_launch_ms, 3), "limits": limits, "pmc_source": source}
 
 
+KEYS = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
+        "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms", "local_rays"]
+
+
 def main():
     args = parse()
     import torch
@@ -311,6 +327,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     # one process per GPU; the gloo rehearsal maps every rank onto the visible devices
     dev = local if args.dist_backend == "nccl" else local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
@@ -319,6 +336,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group("gloo")
+    on_dev = args.dist_backend == "nccl"
 
     extra = []
     for _ in range(args.extra_streams):
@@ -328,75 +346,88 @@ def main():
     torch.cuda.synchronize()
     scene = T.Scene(scene_file(args.scene))
     d_scene = scene.copySceneToDevice(dev)
+    # the per-frame traversal-tree build runs on the host: each process (one per
+    # GPU) takes its share of the cores this host lets it use
+    build_threads = args.build_threads
+    if build_threads == -2:
+        build_threads = max(1, usable_cores()[0] // max(local_world, 1))
+    d_scene.set_build_threads(build_threads)
     W, H = args.width, args.height
     pt = T.PathTracer("", W, H, dev)
     if args.env == "none":
         args.env = None
     if args.env == "sky":
         pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), device=dev)
-    band = (args.band_rows, world, rank)
-    ranks = world
-    if args.emulate_ranks > 1 and world == 1:
-        ranks = args.emulate_ranks
-        band = (args.band_rows, ranks, 0)
-    # weak scaling: a batch of `ranks` frames, frame f with seed + f, each banded across all ranks
-    n_frames = ranks if args.scaling == "weak" else 1
-    seeds = [args.seed + f for f in range(n_frames)]
-    radiances = [torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}") for _ in range(n_frames)]
     flags = args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0)
-
-    build_ms = []
-
-    def step():
-        # doTrace rebuilds the world transform and the BVH every frame (path_tracer.cu:536-542)
-        tb = time.perf_counter()
-        d_scene.build()
-        build_ms.append((time.perf_counter() - tb) * 1e3)
-        st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
-                              radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
-                              refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
-                              lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch)
-        if world == 1:
-            return st, radiances[0]
-        src = radiances if args.dist_backend == "nccl" else [r.cpu() for r in radiances]   # gloo: host tensors
-        if args.scaling == "weak":
-            return st, shard.exchange_frames(src, H, args.band_rows, world, rank)
-        return st, shard.gather_frame(src[0], H, args.band_rows, world, rank)
-
-    for _ in range(args.warmup):
-        step()
+    emulate = args.emulate_ranks if (args.emulate_ranks > 1 and world == 1) else 0
+    ranks = emulate or world
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(args.steps):
-        st, frame = step()
-        stats.append(st)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    def measure(scaling, band_index):
+        """Warm-up + K timed steps of one scaling mode with this process
+        rendering band `band_index` of `ranks`; returns (max-over-ranks
+        elapsed, summed stats over ranks, this rank's stats, build ms, the last
+        step's frame output)."""
+        n_frames = ranks if scaling == "weak" else 1
+        seeds = [args.seed + f for f in range(n_frames)]
+        radiances = [torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}") for _ in range(n_frames)]
+        band = (args.band_rows, ranks, band_index)
+        build_ms = []
 
-    keys = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
-            "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms", "local_rays"]
-    local_tot = {k: float(sum(s[k] for s in stats)) for k in keys}
-    vec = torch.tensor([local_tot[k] for k in keys] + [elapsed], dtype=torch.float64,
-                       device=f"cuda:{dev}" if args.dist_backend == "nccl" else "cpu")
-    if world > 1:
-        mx = vec.clone()
-        dist.all_reduce(vec, op=dist.ReduceOp.SUM)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        elapsed = float(mx[-1].item())
-        tot = {k: float(vec[i].item()) for i, k in enumerate(keys)}
-        tot["trace_ms_max"] = float(mx[keys.index("trace_ms")].item())
-        tot["trace_launches_max"] = float(mx[keys.index("trace_launches")].item())
-    else:
-        tot = dict(local_tot)
-        tot["trace_ms_max"] = tot["trace_ms"]
-        tot["trace_launches_max"] = tot["trace_launches"]
+        def step():
+            # doTrace rebuilds the world transform and the BVH every frame (path_tracer.cu:536-542)
+            tb = time.perf_counter()
+            d_scene.build()
+            build_ms.append((time.perf_counter() - tb) * 1e3)
+            st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
+                                  radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
+                                  refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
+                                  lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch)
+            if world == 1:
+                return st, radiances[0]
+            src = radiances if on_dev else [r.cpu() for r in radiances]   # gloo: host tensors
+            if scaling == "weak":
+                return st, shard.exchange_frames(src, H, args.band_rows, world, rank)
+            return st, shard.gather_frame(src[0], H, args.band_rows, world, rank)
+
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        t0 = time.perf_counter()
+        stats, frame = [], None
+        for _ in range(args.steps):
+            st, frame = step()
+            stats.append(st)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        mine = {k: float(sum(x[k] for x in stats)) for k in KEYS}
+        vec = torch.tensor([mine[k] for k in KEYS] + [elapsed], dtype=torch.float64,
+                           device=f"cuda:{dev}" if on_dev else "cpu")
+        if world > 1:
+            mx = vec.clone()
+            dist.all_reduce(vec, op=dist.ReduceOp.SUM)
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            elapsed = float(mx[-1].item())
+        tot = {k: float(vec[i].item()) for i, k in enumerate(KEYS)}
+        return elapsed, tot, mine, build_ms[-args.steps:], frame, n_frames, seeds
+
+    def measure_all(scaling):
+        """measure() on this process's band, or every emulated rank's in turn
+        (the step of an N-GPU run is its slowest rank's)."""
+        if not emulate:
+            return measure(scaling, rank) + ([],)
+        order = [0] if args.emulate_rank0_only else list(range(emulate))
+        per = [measure(scaling, r) for r in order]
+        slow = max(range(len(per)), key=lambda i: per[i][0])
+        tot = {k: sum(p[1][k] for p in per) for k in KEYS}
+        e, _, mine, bms, frame, nfr, seeds = per[slow]
+        return e, tot, mine, bms, frame, nfr, seeds, [round(p[0] / args.steps * 1e3, 3) for p in per]
+
+    elapsed, tot, local_tot, build_ms, frame, n_frames, seeds, per_rank_ms = measure_all(args.scaling)
 
     def verify(frame):
         """This rank's assembled frame (weak: frame `rank`, seed + rank; strong:
@@ -409,18 +440,30 @@ def main():
         return bool(torch.equal(got.view(torch.int32), full.view(torch.int32)))
 
     verified = None
-    if world > 1 and args.verify_gather and args.scaling == "weak":
-        ok = torch.tensor([1.0 if verify(frame) else 0.0], dtype=torch.float64,
-                          device=f"cuda:{dev}" if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        verified = bool(ok.item() == 1.0)
+    if world > 1 and args.verify_gather:
+        ok = verify(frame) if (args.scaling == "weak" or rank == 0) else True
+        okt = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=f"cuda:{dev}" if on_dev else "cpu")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        verified = bool(okt.item() == 1.0)
+
+    weak = None
+    if ranks > 1 and args.scaling == "strong" and args.weak_extra:
+        we, wt, _, _, _, wnf, _, wper = measure_all("weak")
+        weak = {"value": round(wt["traversals"] / we / 1e6, 2), "unit": "Mrays/s",
+                "ms_per_step": round(we / args.steps * 1e3, 3), "frames_per_step": wnf,
+                "step": f"{wnf} frames (seeds {args.seed}..{args.seed + wnf - 1}), each banded across {ranks} ranks"
+                        + (", RCCL all-to-all" if world > 1 else ""),
+                "msamples_per_s": round(wt["samples"] / we / 1e6, 2)}
+        if wper:
+            weak["per_rank_ms"] = wper
 
     if rank == 0:
         K = args.steps
         rays = tot["traversals"]
         value = rays / elapsed / 1e6
         step_s = elapsed / K
-        # algorithmic bytes of the dominant kernel (k_trace), rank 0's device, per step
+        # algorithmic bytes of the dominant kernel (k_trace), this device (the slowest
+        # emulated rank's), per step
         l_tot = local_tot
         nl = max(l_tot["trace_launches"], 1.0)
         bytes_step = (B_INNER * l_tot["internal_visits"] + B_WIDE * l_tot["wide_visits"] + B_LEAF * l_tot["leaf_tests"]
@@ -428,6 +471,15 @@ def main():
         avg_launch_ms = l_tot["trace_kernel_ms"] / nl   # each launch's own HIP-event time (= rocprof's per dispatch)
         batch = (f" x {n_frames} frames (seeds {seeds[0]}..{seeds[-1]}), each banded across {ranks} ranks"
                  if n_frames > 1 else "")
+        if world > 1:
+            par = (f"pixel-bands x{world} (rows of {args.band_rows}) + "
+                   + ("RCCL " if on_dev else "gloo (1-GPU rehearsal) ")
+                   + ("all-to-all" if args.scaling == "weak" else "gather"))
+        elif emulate:
+            par = (f"1 GPU, rank 0 of {emulate} emulated" if args.emulate_rank0_only else
+                   f"1 GPU, {emulate} ranks emulated in turn (step = slowest rank)")
+        else:
+            par = "1 GPU"
         config = {"workload": f"{args.scene}.gltf {W}x{H} {args.spp}spp depth {args.depth}"
                               + (" env sky" if args.env else "") + (" env-IS" if args.env_is else "") + batch,
                   "scene": f"{args.scene}.gltf", "width": W, "height": H, "spp": args.spp,
@@ -437,10 +489,7 @@ def main():
                   "launch_schedule": ("one launch per frame" if args.pipe_sets == 1 else
                                       f"pipe_sets={args.pipe_sets}" if args.pipe_sets > 1 else "auto"),
                   "lanes_per_pixel": args.lanes_per_pixel or "auto",
-                  "parallelism": f"pixel-bands x{world} (rows of {args.band_rows}) + "
-                                 + ("RCCL " if args.dist_backend == "nccl" else "gloo (1-GPU rehearsal) ")
-                                 + ("all-to-all" if args.scaling == "weak" else "gather")
-                  if world > 1 else ("1 GPU" if ranks == 1 else f"1 GPU, rank 0 of {ranks} emulated")}
+                  "parallelism": par}
         roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms)
         out = {
             "metric": "Mrays/s at 1920x1080x1024spp (box.gltf, 8 bounces); achieved GB/s vs peak",
@@ -466,16 +515,21 @@ def main():
             "visits_per_ray": {k: round(l_tot[k] / max(l_tot["traversals"], 1), 3)
                                for k in ("wide_visits", "internal_visits", "leaf_tests")},
             "roofline": roof,
-            "phases_ms_per_step": {"scene_build": round(sum(build_ms[-K:]) / K, 3),
+            "phases_ms_per_step": {"scene_build": round(sum(build_ms) / K, 3),
                                    "rng_init": round(l_tot["rng_init_ms"] / K, 3),
                                    "trace": round(l_tot["trace_ms"] / K, 3),
                                    "resolve": round(l_tot["resolve_ms"] / K, 3)},
+            "build_threads": build_threads,
         }
-        if world > 1 and args.verify_gather:
+        if per_rank_ms:
+            out["per_rank_ms"] = per_rank_ms
+        if weak is not None:
+            out["weak"] = weak
+        if verified is not None:
             # the assembled frame(s) must equal one GPU rendering every row (the
             # RNG subsequence is the global pixel index, path_tracer.cu:39,320)
-            out["gather_verified"] = verified if args.scaling == "weak" else verify(frame)
-        if world == 1 and args.cpu_baseline:
+            out["gather_verified"] = verified
+        if world == 1 and not emulate and args.cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -76,3 +76,36 @@ def test_full_size_default_order_equals_reference_order(cfg, name, W, H, spp, de
         assert st["samples"] == W * H * spp
     finally:
         d.close()
+
+
+def test_full_size_env_importance_sampling_c3():
+    """C3 with A15 on at its full benchmark size (ball + sky, 1920x1080, 4096
+    spp; BASELINE configs[2] names the importance-sampling path): the default
+    traversal equals the reference's visit order bit for bit with IS on, pair
+    mode (the default) equals one lane per pixel, the ray counts agree, and the
+    framebuffer is copyToFB of the radiance."""
+    W, H, spp, depth = 1920, 1080, 4096, 8
+    s = T.Scene(scene_path("ball"))
+    d = s.copySceneToDevice(0).build()
+    try:
+        pt = T.PathTracer("", W, H, 0)
+        pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), 0)
+        IS = T._lib.FLAG_ENV_IS
+        rad, fb, st = _render(pt, d, s.m_camera, W, H, spp, depth, flags=IS)
+        ref, fbr, str_ = _render(pt, d, s.m_camera, W, H, spp, depth, flags=IS | T._lib.FLAG_REF_ORDER)
+        diff = int((_bits(rad) != _bits(ref)).any(-1).sum())
+        assert diff == 0, diff
+        assert np.array_equal(fb, fbr)
+        assert st["traversals"] == str_["traversals"] and st["shade_hits"] == str_["shade_hits"]
+        one, fb1, st1 = _render(pt, d, s.m_camera, W, H, spp, depth, flags=IS, lanes_per_pixel=1)
+        assert np.array_equal(_bits(one), _bits(rad))
+        assert st1["traversals"] == st["traversals"]
+        plain, _, st0 = _render(pt, d, s.m_camera, W, H, spp, depth)
+        assert st["traversals"] > st0["traversals"]     # the env shadow rays
+        assert np.isfinite(rad).all()
+        q = np.clip(rad * np.float32(255.0), 0.0, 255.0).astype(np.uint8)[::-1]
+        assert np.array_equal(fb[..., 0], q[..., 2]) and np.array_equal(fb[..., 1], q[..., 1])
+        assert np.array_equal(fb[..., 2], q[..., 0])
+        assert st["samples"] == W * H * spp
+    finally:
+        d.close()

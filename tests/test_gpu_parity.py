@@ -280,27 +280,59 @@ def test_pair_mode_full_resolution_c3(built):
     assert st["traversals"] == oc["traversals"]
 
 
-@pytest.mark.parametrize("name", ["ball", "box1", "box"])
-def test_env_importance_sampling_parity(built, name):
+@pytest.mark.parametrize("lanes", [1, 2])
+@pytest.mark.parametrize("name", ["ball", "box1", "box", "square"])
+def test_env_importance_sampling_parity(built, name, lanes):
     """TPT_FLAG_ENV_IS (A15 re-derived, opt-in): env next-event estimation at
     diffuse hits against the oracle's restatement -- same tables, samples,
-    shadow rays and ray counts; and the flag does change the image."""
+    shadow rays and ray counts; and the flag does change the image.  Both lane
+    modes: in pair mode the path lane draws the env sample's uniforms in RNG
+    order and the side lane evaluates it and traces its shadow ray after the
+    bounce's delta-light rays (box1, box: env only; ball, square: a light too)."""
     s, d, o = built[name]
     W, H, spp = 48, 27, 8
     sky = T.procedural_sky(128, 64)
     pt = T.PathTracer("", W, H, 0)
     pt.envLight = T.EnvLight(sky, 0)
     rad = np.zeros((H, W, 3), np.float32)
-    stats = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=rad, flags=T._lib.FLAG_ENV_IS)
+    stats = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=rad, flags=T._lib.FLAG_ENV_IS,
+                       lanes_per_pixel=lanes)
     orad, _, oc = O.render(o, W, H, spp, 8, 42, env=sky[::-1].copy(), trig_mode=1, env_is=True)
     m = image_metrics(rad, orad)
     assert_parity(m)
-    if m["bit_same"] == 1.0:
-        assert stats["traversals"] == oc["traversals"]
+    assert m["bit_same"] == 1.0, m
+    assert stats["traversals"] == oc["traversals"]
     plain = np.zeros((H, W, 3), np.float32)
     st2 = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=plain)
     assert st2["traversals"] < stats["traversals"]        # one env shadow ray per diffuse hit
     assert not np.array_equal(_bits(plain), _bits(rad))
+    ref = np.zeros((H, W, 3), np.float32)                  # the reference's visit order, IS on
+    st3 = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=ref,
+                     flags=T._lib.FLAG_ENV_IS | T._lib.FLAG_REF_ORDER)
+    assert np.array_equal(_bits(ref), _bits(rad))
+    assert st3["traversals"] == stats["traversals"]
+
+
+def test_env_importance_sampling_full_resolution_c3(built):
+    """C3 with A15 on (BASELINE configs[2] "env-light importance sampling
+    path"): ball + the 2048x1024 sky at 1920x1080, 2 spp, bit-exact against the
+    oracle's restatement in both lane modes (pair mode is the default)."""
+    s, d, o = built["ball"]
+    W, H, spp = 1920, 1080, 2
+    sky = T.procedural_sky(2048, 1024)
+    orad, obgra, oc = O.render(o, W, H, spp, 8, 42, env=sky[::-1].copy(), trig_mode=1, env_is=True)
+    pt = T.PathTracer("", W, H, 0)
+    pt.envLight = T.EnvLight(sky, 0)
+    for lanes in (0, 1, 2):
+        fb = np.zeros((H, W, 4), np.uint8)
+        rad = np.zeros((H, W, 3), np.float32)
+        st = pt.doTrace(d, s.m_camera, fb, spp, seed=42, radiance=rad, flags=T._lib.FLAG_ENV_IS,
+                        lanes_per_pixel=lanes)
+        m = image_metrics(rad, orad)
+        assert m["bit_same"] == 1.0, (lanes, m)
+        assert np.array_equal(fb[..., :3], obgra[..., :3]), lanes
+        assert st["traversals"] == oc["traversals"], lanes
+        assert st["shade_hits"] == oc["shade_hits"], lanes
 
 
 def test_band_sharding_bit_identical(built):

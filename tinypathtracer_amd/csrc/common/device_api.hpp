@@ -64,6 +64,12 @@ struct TraceArgs {
     const float* is_row;                 //   row sums [h]
     const float* is_marg;                //   marginal prefix over rows [h]
     float is_total;
+    // guide tables of the two searches (exact lower_bound in few dependent loads):
+    // is_guide_r[k] = lower_bound(is_marg, (k / kr) * is_total), k = 0..kr;
+    // is_guide_c[iy * (kc + 1) + k] = lower_bound(row iy of is_cond, (k / kc) * is_row[iy])
+    const int32_t* is_guide_r;
+    const int32_t* is_guide_c;
+    int32_t is_kr, is_kc;                // powers of two
     int32_t env_is;                      // TPT_FLAG_ENV_IS and a non-empty distribution
     // camera
     float c2w[16];

@@ -136,6 +136,8 @@ struct tpt_env {
     // prefix sums, row sums, marginal prefix over rows; total <= 0 disables
     DevBuf<float> is_w, is_cond, is_row, is_marg;
     float is_total = 0.0f;
+    DevBuf<int32_t> is_guide_r, is_guide_c;   // guide tables of the two CDF searches (trace.hip lower_bound_guided)
+    int32_t is_kr = 1, is_kc = 1;
 };
 
 namespace {
@@ -171,6 +173,26 @@ void build_env_is(const uint8_t* rgba, int w, int h, std::vector<float>& W, std:
         marg[iy] = acc_rows;
     }
     total = acc_rows;
+}
+
+// Guide table of a nondecreasing prefix array a[0, n) with last entry `total`:
+// g[k] = lower_bound(a, fl((k / K) * total)) for k = 0..K (trace.hip
+// lower_bound_guided).  The thresholds are computed in float exactly as the
+// kernel's t = x * total is, so the guided search returns the plain search's index.
+void build_guide(const float* a, int n, float total, int K, int32_t* g) {
+    const float inv = 1.0f / (float)K;   // exact: K is a power of two
+    int i = 0;
+    for (int k = 0; k <= K; ++k) {
+        const float thr = ((float)k * inv) * total;
+        while (i < n - 1 && a[i] < thr) ++i;
+        g[k] = i;
+    }
+}
+
+int pow2_at_least(int n) {
+    int k = 1;
+    while (k < n && k < (1 << 20)) k <<= 1;
+    return k;
 }
 
 }  // namespace
@@ -698,6 +720,16 @@ tpt_status tpt_env_create(const uint8_t* rgba, int32_t w, int32_t h, int device,
     if (e == hipSuccess) e = env->is_cond.upload(icond.data(), icond.size(), nullptr);
     if (e == hipSuccess) e = env->is_row.upload(irow.data(), irow.size(), nullptr);
     if (e == hipSuccess) e = env->is_marg.upload(imarg.data(), imarg.size(), nullptr);
+    {   // guide tables: rows at the row count, columns at a quarter of the row length
+        env->is_kr = pow2_at_least(h);
+        env->is_kc = pow2_at_least(std::max(1, w / 4));
+        std::vector<int32_t> gr((size_t)env->is_kr + 1), gc((size_t)h * (env->is_kc + 1));
+        build_guide(imarg.data(), h, env->is_total, env->is_kr, gr.data());
+        for (int iy = 0; iy < h; ++iy)
+            build_guide(icond.data() + (size_t)iy * w, w, irow[iy], env->is_kc, gc.data() + (size_t)iy * (env->is_kc + 1));
+        if (e == hipSuccess) e = env->is_guide_r.upload(gr.data(), gr.size(), nullptr);
+        if (e == hipSuccess) e = env->is_guide_c.upload(gc.data(), gc.size(), nullptr);
+    }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         delete env;
@@ -780,6 +812,10 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.is_row = env ? env->is_row.p : nullptr;
     a.is_marg = env ? env->is_marg.p : nullptr;
     a.is_total = env ? env->is_total : 0.0f;
+    a.is_guide_r = env ? env->is_guide_r.p : nullptr;
+    a.is_guide_c = env ? env->is_guide_c.p : nullptr;
+    a.is_kr = env ? env->is_kr : 1;
+    a.is_kc = env ? env->is_kc : 1;
     if (cam) {
         std::memcpy(a.c2w, cam->c2w, sizeof a.c2w);
         float r[4];
@@ -869,17 +905,19 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     if (p->lanes_per_pixel < 0 || p->lanes_per_pixel > 2) return fail(TPT_ERR_INVALID_ARG, "lanes_per_pixel: 0, 1 or 2");
     // auto: pair mode wherever there are shadow rays to hand off (C3 1080p 4096 spp:
     // 4.91 -> 6.65 Grays/s); the kernel falls back to one lane per pixel otherwise
-    a.pair = (p->lanes_per_pixel == 2 || (p->lanes_per_pixel == 0 && s->n_lights > 0)) ? 1 : 0;
+    // (A15 env IS: the env shadow ray of every diffuse bounce is the side lane's job too)
+    a.pair = (p->lanes_per_pixel == 2 || (p->lanes_per_pixel == 0 && (s->n_lights > 0 || a.env_is))) ? 1 : 0;
     // Refill: a wave leaves its traversal loop to shade once fewer than this many
     // lanes still traverse.  A shading pass costs ~5 node steps, so passes are
     // batched; in pair mode half the lanes (the side lanes) are mostly idle and
     // the threshold scales down with them (C3 1080p 4096 spp: 24 -> 5.88,
     // 8 -> 6.44, 2..12 within 6.2-6.6 Grays/s; C2 single-lane: 16-24 best).
-    const bool pair_kernel = a.pair && s->n_lights > 0 && (s->n_materials + 1) < 0x7fff;
+    const bool pair_kernel = a.pair && (s->n_lights > 0 || a.env_is) && (s->n_materials + 1) < 0x7fff &&
+                             !(p->flags & TPT_FLAG_REF_ORDER);
     // the trace grid's y extent is (band row blocks) x frames: 8-row workgroups in
     // pair mode, 16 otherwise (launch_trace)
     {
-        const int wg_rows = (pair_kernel && !a.env_is && !(p->flags & TPT_FLAG_REF_ORDER)) ? 8 : 16;
+        const int wg_rows = pair_kernel ? 8 : 16;
         if ((size_t)((bh + wg_rows - 1) / wg_rows) * nf > 65535)
             return fail(TPT_ERR_INVALID_ARG, "frame batch too large for one launch");
     }

@@ -53,6 +53,20 @@
 #ifndef TPT_TRACE_WAVES
 #define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator
 #endif
+#ifndef TPT_TRACE_WAVES_IS
+// The env importance-sampling variants (A15) carry the env sample's state across
+// the shading pass: at 96 VGPRs (5 waves) they spilled 121 VGPRs to scratch;
+// 4 waves give them 128.
+#define TPT_TRACE_WAVES_IS 4
+#endif
+#ifndef TPT_TRACE_WAVES_PAIR
+// pair-mode (delta-light) variants: at 5 waves (96 VGPRs) they spilled 38 VGPRs;
+// C3 4096 spp, 4 waves: +6.4 % (7,220 -> 7,685 Mrays/s, 2 interleaved reps)
+#define TPT_TRACE_WAVES_PAIR 4
+#endif
+#ifndef TPT_ENV_INLINE
+#define TPT_ENV_INLINE 0   // 1: env_lookup inlined in every variant (A/B builds)
+#endif
 
 namespace tpt {
 
@@ -587,9 +601,7 @@ __device__ __forceinline__ void light_sample(const DevLight* __restrict__ Ls, in
 
 // sampleEnvLights (:288-294): Vec2UV (env_light.cuh:72-78) + point/clamp fetch
 // (texture.cu:156-170) of the RGBA8 equirect, row 0 = bottom.
-// (kept out of line: inlined, its double-precision trig raised the register
-// pressure of the whole kernel; C3 measured 17 % slower)
-__device__ __noinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
+__device__ __forceinline__ V3 env_lookup_inl(const uint32_t* __restrict__ env, int w, int h, V3 d) {
     float u = patan2_fast(d.z, d.x) / (2.0f * kPi);
     if (u < 0.0f) u += 1.0f;
     const float v = 1.0f - pacos_fast(fclamp(d.y, 1.0f, -1.0f)) / kPi;
@@ -599,6 +611,19 @@ __device__ __noinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w, i
     iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
     const uint32_t t = env[(size_t)iy * (size_t)w + (size_t)ix];
     return (1.0f / 255.0f) * v3((float)(t & 0xffu), (float)((t >> 8) & 0xffu), (float)((t >> 16) & 0xffu));
+}
+// Out of line in the variants without env importance sampling: inlined, its
+// double-precision trig raised the register pressure of the whole kernel (C3
+// 17 % slower at 5 waves; at 4 waves, 128 VGPRs, within 1-3 %).  The A15
+// variants inline it (and env_is_sample): C3 with IS +25 % -- the calls'
+// register saves went to scratch.
+__device__ __noinline__ V3 env_lookup_call(const uint32_t* __restrict__ env, int w, int h, V3 d) {
+    return env_lookup_inl(env, w, h, d);
+}
+template <bool INLINE>
+__device__ __forceinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
+    if constexpr (INLINE || TPT_ENV_INLINE) return env_lookup_inl(env, w, h, d);
+    else return env_lookup_call(env, w, h, d);
 }
 
 __device__ __forceinline__ int band_row(int ly, int band_rows, int band_count, int band_index) {
@@ -621,27 +646,47 @@ enum : int { PH_CAMERA = 0, PH_EXT = 1, PH_SHADOW = 2, PH_PROBE = 3, PH_ENVSHADO
 // factor Le * cos / (pi * pdf) for a diffuse hit with incident-side normal nf,
 // or false when the sample cannot contribute (the two uniforms are drawn
 // either way).  The oracle's env_is_sample is the same arithmetic.
-__device__ __forceinline__ int lower_bound_f(const float* __restrict__ a, int n, float t) {
-    int lo = 0, hi = n - 1;   // first i with a[i] >= t (n - 1 if none)
-    while (lo < hi) {
+// lower_bound (first i with a[i] >= t; n - 1 if none) of t = x * total over a
+// nondecreasing prefix array a[0, n) whose last entry is total, through a guide
+// table: g[k] = lower_bound(a, fl((k / K) * total)), k = 0..K, K a power of two.
+// k = floor(x * K) is exact (a power-of-two scale) and x >= k / K, so t >=
+// fl((k / K) * total) by monotone rounding: every a[j] with j < g[k] is < t, and
+// the answer lies in [g[k], g[k + 1]].  The same index as a plain binary search
+// over the whole array (the oracle's), in about two dependent loads instead of
+// log2(n): the range's entries are loaded together and counted.
+__device__ __forceinline__ int lower_bound_guided(const float* __restrict__ a, int n, float t, float x,
+                                                  const int32_t* __restrict__ g, int K) {
+    int k = (int)(x * (float)K);
+    k = k < 0 ? 0 : (k > K ? K : k);
+    int lo = g[k];
+    int hi = k < K ? g[k + 1] : n - 1;
+    hi = hi > n - 1 ? n - 1 : hi;
+    while (hi - lo > 8) {   // rare: a bucket spanning many entries of tiny weight
         const int mid = (lo + hi) >> 1;
         if (a[mid] >= t) hi = mid;
         else lo = mid + 1;
     }
-    return lo;
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int i = lo + j;
+        const float v = i < hi ? a[i] : t;
+        cnt += v < t ? 1 : 0;
+    }
+    return lo + cnt;
 }
 
-__device__ __noinline__ bool env_is_sample(const TraceArgs& a, V3 nf, uint32_t st[6], V3& dir, V3& k_le) {
-    const float x1 = xorwow_uniform(st);
-    const float x2 = xorwow_uniform(st);
+// x1, x2: the two uniforms, drawn by the pixel's path lane in RNG order (pair
+// mode hands them to the side lane with the bounce's shadow job).
+__device__ __forceinline__ bool env_is_sample(const TraceArgs& a, V3 nf, float x1, float x2, V3& dir, V3& k_le) {
     const int W = a.env_w, H = a.env_h;
     const float t1 = x1 * a.is_total;
-    const int iy = lower_bound_f(a.is_marg, H, t1);
+    const int iy = lower_bound_guided(a.is_marg, H, t1, x1, a.is_guide_r, a.is_kr);
     const float lo1 = iy > 0 ? a.is_marg[iy - 1] : 0.0f;
     const float f1 = fminf((t1 - lo1) / (a.is_marg[iy] - lo1), 0.99999994f);
     const float* cond = a.is_cond + (size_t)iy * (size_t)W;
     const float t2 = x2 * a.is_row[iy];
-    const int ix = lower_bound_f(cond, W, t2);
+    const int ix = lower_bound_guided(cond, W, t2, x2, a.is_guide_c + (size_t)iy * (size_t)(a.is_kc + 1), a.is_kc);
     const float lo2 = ix > 0 ? cond[ix - 1] : 0.0f;
     const float f2 = fminf((t2 - lo2) / (cond[ix] - lo2), 0.99999994f);
     const float u = ((float)ix + f2) / (float)W;
@@ -654,7 +699,7 @@ __device__ __noinline__ bool env_is_sample(const TraceArgs& a, V3 nf, uint32_t s
     const float pdf = ((a.is_w[(size_t)iy * (size_t)W + ix] / a.is_total) * ((float)W * (float)H)) /
                       ((2.0f * kPi * kPi) * sth);
     if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < kRealMax)) return false;
-    const V3 le = env_lookup(a.env, W, H, dir);
+    const V3 le = env_lookup<true>(a.env, W, H, dir);
     const float k = c / (kPi * pdf);
     k_le = k * le;
     return true;
@@ -786,8 +831,9 @@ struct PathRecords {
 // instead of 1 + lights, which is what bounds tail-heavy frames (C3).
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
           bool PAIR = false>
-__global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
-    static_assert(!PAIR || (ORDERED && LIGHTS && !ENVIS), "pair mode: ordered delta-light variants");
+__global__ __launch_bounds__(256, ENVIS ? TPT_TRACE_WAVES_IS : (PAIR ? TPT_TRACE_WAVES_PAIR : TPT_TRACE_WAVES))
+void k_trace(TraceArgs a) {
+    static_assert(!PAIR || (ORDERED && LIGHTS), "pair mode: ordered variants with 5-word records");
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // grid y interleaves the frames of a batch: consecutive workgroups render the
@@ -877,6 +923,10 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     uint32_t mk = 0;   // material id | p-kind << 30 of the current bounce
     bool env_pending = false;   // A15: this bounce's env next-event sample is still to be drawn
     V3 env_k = v3(0.0f, 0.0f, 0.0f);
+    // pair mode + A15: the env sample's uniforms and incident-side normal, drawn by
+    // the path lane when it posts the bounce's shadow job (side lane: as received)
+    float env_x1 = 0.0f, env_x2 = 0.0f;
+    V3 env_nf = v3(0.0f, 0.0f, 0.0f);
     V3 rd = v3(0.0f, 0.0f, 0.0f), nd = rd, nrm = rd, direct = rd;
     Trav r;
     trav_begin(r, rd, v3(1.0f, 1.0f, 1.0f), TM_CLOSEST);
@@ -891,6 +941,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
     // while waiting for the partner, a job to post at the next exchange.  Side
     // lane: the level it works on and the direct sum it hands back.
     bool delegated = false, post = false, ready = false;   // (partner idle <=> pend < 0)
+    bool post_env = false;   // the posted job carries an env sample (A15)
     int pend = -1, jlevel = 0;
     // (the unwind's seed while the path lane waits for its side lane lives in
     // `direct`: the path's levels are all recorded by then)
@@ -980,7 +1031,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
             if (phase == PH_EXT) {
                 if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
-                    if (a.env) L = env_lookup(a.env, a.env_w, a.env_h, rd);
+                    if (a.env) L = env_lookup<ENVIS>(a.env, a.env_w, a.env_h, rd);
                     finish = true;
                 } else {           // hit shading prelude (:364-381)
                     ++c_shade;
@@ -1031,7 +1082,7 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             TPT_SEC(1)
             V3 td = rd;
             bool shadow = false;
-            if (PAIR && lights_next && !side && li == 0 && pend < 0) {
+            if (PAIR && lights_next && !side && li == 0 && pend < 0 && (a.n_lights > 0 || (ENVIS && env_pending))) {
                 // hand this bounce's shadow rays to the idle side lane (posted at the
                 // exchange below: origin r.o, material mk, level depth)
                 post = true;
@@ -1039,8 +1090,18 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 pend = depth;
                 delegated = true;
                 li = a.n_lights;
+                if (ENVIS && env_pending) {
+                    // A15: the env sample's two uniforms are this lane's to draw, after
+                    // the extension direction and before the probe's (RNG order); the
+                    // side lane evaluates the sample and traces its shadow ray
+                    env_pending = false;
+                    env_x1 = xorwow_uniform(st);
+                    env_x2 = xorwow_uniform(st);
+                    env_nf = (dot(rd, nrm) > 0.0f ? -1.0f : 1.0f) * nrm;   // getNewDirection's flip
+                    post_env = true;
+                }
             }
-            if (PAIR && lights_next && side && li >= a.n_lights) {
+            if (PAIR && lights_next && side && li >= a.n_lights && !(ENVIS && env_pending)) {
                 // the side lane's job is done: its direct sum goes back at the exchange
                 ready = true;
                 ts = TS_IDLE;
@@ -1057,14 +1118,23 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                     bool env_ray = false;
                     if (ENVIS && env_pending) {   // after the delta lights, before the probe
                         env_pending = false;
-                        const V3 nf = (dot(rd, nrm) > 0.0f ? -1.0f : 1.0f) * nrm;   // getNewDirection's flip
-                        if (env_is_sample(a, nf, st, td, env_k)) {
+                        V3 nf = env_nf;
+                        float x1 = env_x1, x2 = env_x2;
+                        if (!(PAIR && side)) {
+                            nf = (dot(rd, nrm) > 0.0f ? -1.0f : 1.0f) * nrm;   // getNewDirection's flip
+                            x1 = xorwow_uniform(st);
+                            x2 = xorwow_uniform(st);
+                        }
+                        if (env_is_sample(a, nf, x1, x2, td, env_k)) {
                             phase = PH_ENVSHADOW;
                             shadow = true;
                             env_ray = true;
                         }
                     }
                     if (env_ray) {
+                    } else if (PAIR && side) {   // the env sample cannot contribute: the job is done
+                        ready = true;
+                        ts = TS_IDLE;
                     } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
                         float af2;
                         new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
@@ -1206,6 +1276,19 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
             const int jpost = __shfl_xor((int)post, 1, 64);
             const float jx = __shfl_xor(r.o.x, 1, 64), jy = __shfl_xor(r.o.y, 1, 64), jz = __shfl_xor(r.o.z, 1, 64);
             const int jmk = __shfl_xor((int)mk, 1, 64), jl = __shfl_xor(jlevel, 1, 64);
+            bool jenv = false;
+            if constexpr (ENVIS) {   // A15: the env sample's uniforms and normal travel with the job
+                jenv = __shfl_xor((int)post_env, 1, 64) != 0;
+                const float e1 = __shfl_xor(env_x1, 1, 64), e2 = __shfl_xor(env_x2, 1, 64);
+                const float n0 = __shfl_xor(env_nf.x, 1, 64), n1 = __shfl_xor(env_nf.y, 1, 64),
+                            n2 = __shfl_xor(env_nf.z, 1, 64);
+                if (side && jpost) {
+                    env_pending = jenv;
+                    env_x1 = e1;
+                    env_x2 = e2;
+                    env_nf = v3(n0, n1, n2);
+                }
+            }
             if (side && jpost) {
                 mk = (uint32_t)jmk;
                 jlevel = jl;
@@ -1213,17 +1296,33 @@ __global__ __launch_bounds__(256, TPT_TRACE_WAVES) void k_trace(TraceArgs a) {
                 direct = v3(0.0f, 0.0f, 0.0f);
                 V3 ldir, lrad;
                 const V3 jo = v3(jx, jy, jz);
-                light_sample(a.lights, 0, jo, ldir, lrad);
-                ++c_trav;
-                trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root, a.cull_eps);
-                phase = PH_SHADOW;
-                ts = TS_TRAV;
-                sl_pend = true;
+                bool go = true;
+                if (a.n_lights > 0) {
+                    light_sample(a.lights, 0, jo, ldir, lrad);
+                    phase = PH_SHADOW;
+                } else if (ENVIS && env_pending) {   // env only: the sample, then its shadow ray
+                    env_pending = false;
+                    go = env_is_sample(a, env_nf, env_x1, env_x2, ldir, env_k);
+                    phase = PH_ENVSHADOW;
+                } else {
+                    go = false;
+                }
+                if (go) {
+                    ++c_trav;
+                    trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root, a.cull_eps);
+                    ts = TS_TRAV;
+                    sl_pend = true;
 #ifdef TPT_VERIFY_CULL
-                vpend = true;
+                    vpend = true;
 #endif
+                } else {   // nothing to trace: the direct sum (zero) goes back at once
+                    r.o = jo;
+                    ready = true;
+                    ts = TS_IDLE;
+                }
             }
             post = false;
+            post_env = false;
             // side -> path: the level's direct sum, in light order
             const int jready = __shfl_xor((int)ready, 1, 64);
             const float dx = __shfl_xor(direct.x, 1, 64), dy = __shfl_xor(direct.y, 1, 64),
@@ -1555,27 +1654,30 @@ static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s)
 // INL: probe pass 1 in the shading pass (an emissive tree of one node); its own
 // variant, so scenes with larger emitter sets keep the leaner kernel.  PAIR:
 // pair mode (delta-light scenes only).
-template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false>
+template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false, bool ENVIS = false>
 static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
     if (a.emit_inline) {
-        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, false, true, PAIR>(a, grid, lds, s);
-        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, false, true, PAIR>(a, grid, lds, s);
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR>(a, grid, lds, s);
     } else {
-        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, false, false, PAIR>(a, grid, lds, s);
-        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, false, false, PAIR>(a, grid, lds, s);
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR>(a, grid, lds, s);
     }
 }
 
 // LDS per 256-lane workgroup: [material table][traversal stack][path records],
 // within kLdsBudget (TPT_TRACE_WAVES workgroups per CU share the 160 KiB).
 constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
+constexpr size_t kLdsBudgetIS = (163840 / TPT_TRACE_WAVES_IS) & ~(size_t)255;
+constexpr size_t kLdsBudgetPair = (163840 / TPT_TRACE_WAVES_PAIR) & ~(size_t)255;
 #ifndef TPT_MTL_LDS_MAX
 #define TPT_MTL_LDS_MAX 2048
 #endif
 constexpr size_t kLdsMtlMax = TPT_MTL_LDS_MAX;   // material tables up to 64 entries go to LDS
 constexpr size_t kLdsNodesMax = TPT_LDS_NODES_MAX;
 
-size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide, int rec_cols = 256) {
+size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide, int rec_cols = 256,
+                       size_t lds_budget = kLdsBudget) {
     // [material table][top 4-wide nodes][traversal stack][path records].
     // Priorities (measured on box): the whole stack (a
     // stack capped at 23 of its 40 slots cost 7 %), then path records up to
@@ -1584,7 +1686,7 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
     const size_t mtl_bytes = mtl_lds ? ((size_t)(a.n_materials + 1) * 2 * 16 + 127) / 128 * 128 : 0;
     a.mtl_in_lds = mtl_lds ? 1 : 0;
     a.lds_mtl_offset = 0;
-    const size_t budget = kLdsBudget - mtl_bytes;
+    const size_t budget = lds_budget - mtl_bytes;
     const size_t slot = 256 * elem;
     const size_t level = (size_t)words * (size_t)rec_cols * sizeof(float);
     // The whole stack (capacity + 3 spare slots for the unconditional 4-wide
@@ -1624,24 +1726,40 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     if (a.flags & TPT_FLAG_REF_ORDER) {
         // the reference's visit order (tests, diagnostics): one general variant
         const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, false);
-        launch_one<64, false, true, false, int>(a, grid, lds, s);
-        return hipGetLastError();
-    }
-    if (a.env_is) {
-        // opt-in env next-event estimation (A15): one general variant (delta
-        // lights machinery, 32-bit stack, any depth) keeps the others lean
-        const size_t lds = trace_lds_bytes(a, 5, sizeof(int), false, true);
-        launch_one<64, true, true, false, int, true>(a, grid, lds, s);
+        if (a.env_is) launch_one<64, false, true, false, int, true>(a, grid, lds, s);
+        else launch_one<64, false, true, false, int>(a, grid, lds, s);
         return hipGetLastError();
     }
     const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
+    const bool mtl_lds_ok = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
+    if (a.env_is) {
+        // opt-in env next-event estimation (A15): variants of their own (the
+        // delta-light machinery: 5-word records), so the others stay lean; pair
+        // mode hands each diffuse bounce's env shadow ray (and its delta lights'
+        // rays) to the side lane
+        const bool pair_is = a.pair && (a.n_materials + 1) < (int)kNoProbe;
+        if (pair_is) grid.y = ((a.band_height + 7) / 8) * (a.n_frames > 0 ? a.n_frames : 1);
+        const size_t lds = trace_lds_bytes(a, 5, small ? 2 : 4, mtl_lds_ok, true, pair_is ? 128 : 256, kLdsBudgetIS);
+#define TPT_IS_LAUNCH(MTL, ST)                                                         \
+    {                                                                                  \
+        if (pair_is) launch_ordered<true, MTL, ST, true, true>(a, grid, lds, s);        \
+        else launch_ordered<true, MTL, ST, false, true>(a, grid, lds, s);               \
+    }
+        if (mtl_lds_ok) {
+            if (small) TPT_IS_LAUNCH(true, uint16_t) else TPT_IS_LAUNCH(true, int)
+        } else {
+            if (small) TPT_IS_LAUNCH(false, uint16_t) else TPT_IS_LAUNCH(false, int)
+        }
+#undef TPT_IS_LAUNCH
+        return hipGetLastError();
+    }
     const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
     const bool mtl_lds = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
     // pair mode: delta lights (shadow rays to hand off), packed probe ids
     const bool pair = a.pair && lights && a.n_lights > 0 && (a.n_materials + 1) < (int)kNoProbe;
     if (pair) {
         grid.y = ((a.band_height + 7) / 8) * (a.n_frames > 0 ? a.n_frames : 1);   // 16x8 pixels per workgroup
-        const size_t lds = trace_lds_bytes(a, 5, small ? 2 : 4, mtl_lds, true, 128);
+        const size_t lds = trace_lds_bytes(a, 5, small ? 2 : 4, mtl_lds, true, 128, kLdsBudgetPair);
         if (mtl_lds) {
             if (small) launch_ordered<true, true, uint16_t, true>(a, grid, lds, s);
             else launch_ordered<true, true, int, true>(a, grid, lds, s);
