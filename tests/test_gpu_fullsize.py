@@ -109,3 +109,25 @@ def test_full_size_env_importance_sampling_c3():
         assert st["samples"] == W * H * spp
     finally:
         d.close()
+
+
+def test_full_size_c2_strong_split_bit_identical():
+    """C2 at full size split 8 ways in interleaved 16-row bands (the strong-scaled
+    multi-GPU split, bench.py --scaling strong): each band set is a drained
+    launch (the latency-oriented DRAIN kernel variants, refill 4), and the
+    assembled frame equals the one-GPU frame bit for bit, with the same rays."""
+    W, H, spp, depth = 1920, 1080, 1024, 8
+    s = T.Scene(scene_path("box"))
+    d = s.copySceneToDevice(0).build()
+    try:
+        pt = T.PathTracer("", W, H, 0)
+        full, _, st = _render(pt, d, s.m_camera, W, H, spp, depth)
+        acc = np.zeros((H, W, 3), np.float32)
+        rays = 0
+        for r in range(8):
+            st_r = pt.doTrace(d, s.m_camera, None, spp, seed=42, max_depth=depth, radiance=acc, band=(16, 8, r))
+            rays += st_r["traversals"]
+        assert int((_bits(acc) != _bits(full)).any(-1).sum()) == 0
+        assert rays == st["traversals"]
+    finally:
+        d.close()

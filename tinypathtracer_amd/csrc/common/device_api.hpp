@@ -95,6 +95,7 @@ struct TraceArgs {
     int32_t n_sliver_groups;             // 0: no sliver triangles
     float cull_eps;                      // absolute position slack of the t-culls (trace.hip "Culling")
     int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
+    int32_t drained;                     // 1: the launch cannot fill the chip (latency-oriented DRAIN variants)
     int32_t xcd_run;                     // > 0: workgroup tiles dealt to XCDs in runs of this many (k_trace)
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS

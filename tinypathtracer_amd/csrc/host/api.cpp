@@ -933,6 +933,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // 84.6 Grays/s vs 24 72.6-78.9; box (1,932) 16 = 24; C5 (131 K) 16 -3 %.
     const int full = s->n_faces <= 4096 ? 16 : 24;
     a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : (drained ? 4 : full));
+    a.drained = drained ? 1 : 0;   // latency-oriented kernel variants (trace.hip DRAIN)
     // Parked-leaf batch (speculative leaf postponement): a wave runs its triangle
     // tests once this many lanes are blocked on a parked leaf.  Pair mode has
     // half the path lanes and its heavy waves few traversing lanes, so it

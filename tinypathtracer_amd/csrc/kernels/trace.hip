@@ -53,6 +53,7 @@
 #ifndef TPT_TRACE_WAVES
 #define TPT_TRACE_WAVES 5   // min waves per SIMD requested from the register allocator
 #endif
+
 #ifndef TPT_TRACE_WAVES_IS
 // The env importance-sampling variants (A15) carry the env sample's state across
 // the shading pass: at 96 VGPRs (5 waves) they spilled 121 VGPRs to scratch;
@@ -403,9 +404,8 @@ __device__ __forceinline__ float cull_slack(const V3& inv, float cull_eps) {
     return cull_eps * fmaxf(fmaxf(fabsf(inv.x), fabsf(inv.y)), fabsf(inv.z));
 }
 template <bool ORDERED>
-__device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos, float cull_eps) {
-    const float4* tr = tri + 3 * pos;
-    const float4 q0 = tr[0], q1 = tr[1], q2 = tr[2];
+__device__ __forceinline__ bool leaf_test_q(Trav& r, const float4 q0, const float4 q1, const float4 q2, int pos,
+                                            float cull_eps) {
     const V3 v0 = v3(q0.x, q0.y, q0.z), e1 = v3(q1.x, q1.y, q1.z), e2 = v3(q2.x, q2.y, q2.z);
     float t, u, v;
     const bool inside = tri_core(r.o, r.d, v0, e1, e2, t, u, v);
@@ -420,6 +420,11 @@ __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tr
     const bool occl = r.mode == TM_OCCL;
     r.mode = (take & occl) ? TM_OCCLUDED : r.mode;
     return take & ((r.mode == TM_ANY) | occl);
+}
+template <bool ORDERED>
+__device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos, float cull_eps) {
+    const float4* tr = tri + 3 * pos;
+    return leaf_test_q<ORDERED>(r, tr[0], tr[1], tr[2], pos, cull_eps);
 }
 
 // Probe pass 1 over an emissive-triangle tree that is a single 4-wide node of
@@ -830,7 +835,7 @@ struct PathRecords {
 // bit-identical.  A pixel's sample chain then pays one traversal per bounce
 // instead of 1 + lights, which is what bounds tail-heavy frames (C3).
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
-          bool PAIR = false>
+          bool PAIR = false, bool DRAIN = false>
 __global__ __launch_bounds__(256, ENVIS ? TPT_TRACE_WAVES_IS : (PAIR ? TPT_TRACE_WAVES_PAIR : TPT_TRACE_WAVES))
 void k_trace(TraceArgs a) {
     static_assert(!PAIR || (ORDERED && LIGHTS), "pair mode: ordered variants with 5-word records");
@@ -935,6 +940,11 @@ void k_trace(TraceArgs a) {
     bool vpend = false;   // a traversal of this lane awaits verification
 #endif
     bool sl_pend = false;   // a traversal of this lane awaits the sliver pass
+    // DRAIN variants (launches too small to fill the chip, where each wave's
+    // chain latency is the frame time): a parked leaf's triangle is loaded when
+    // the leaf is parked, in flight while the walk goes on (strong-scaled C2,
+    // rank 0 of 8: -5 % time; C5 at full occupancy +5 %, so only these variants)
+    float4 pq0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pq1 = pq0, pq2 = pq0;
     const int refill = a.refill;
     // pair mode state.  Path lane: partner idle?, the level whose shadow rays the
     // partner holds (-1: none), this level's shadows delegated?, the unwind's seed
@@ -1389,6 +1399,12 @@ void k_trace(TraceArgs a) {
                 if (r.node >= nint && r.pend < 0) {
                     r.pend = r.node - nint;
                     r.node = r.sp == 0 ? -1 : stk.get(--r.sp);
+                    if constexpr (DRAIN) {
+                        const float4* tr = a.tri + 3 * r.pend;   // in flight while the walk goes on
+                        pq0 = tr[0];
+                        pq1 = tr[1];
+                        pq2 = tr[2];
+                    }
                 }
                 has = r.pend >= 0;
                 inner_ready = r.node >= 0 && r.node < nint;
@@ -1400,7 +1416,9 @@ void k_trace(TraceArgs a) {
                                 __ballot(inner_ready) == 0ull;
                 if (go && has) {
                     ++c_leaf;
-                    if (leaf_test<ORDERED>(r, a.tri, r.pend, a.cull_eps)) {
+                    const bool stop = DRAIN ? leaf_test_q<ORDERED>(r, pq0, pq1, pq2, r.pend, a.cull_eps)
+                                            : leaf_test<ORDERED>(r, a.tri, r.pend, a.cull_eps);
+                    if (stop) {
                         r.node = -1;
                         r.sp = 0;
                     }
@@ -1646,23 +1664,36 @@ hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipSt
 }
 
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
-          bool PAIR = false>
+          bool PAIR = false, bool DRAIN = false>
 static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR>), grid, dim3(256), lds, s, a);
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR, DRAIN>), grid, dim3(256), lds,
+                       s, a);
 }
 
 // INL: probe pass 1 in the shading pass (an emissive tree of one node); its own
 // variant, so scenes with larger emitter sets keep the leaner kernel.  PAIR:
 // pair mode (delta-light scenes only).
+template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false, bool ENVIS = false, bool DRAIN = false>
+static void launch_ordered_d(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (a.emit_inline) {
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR, DRAIN>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR, DRAIN>(a, grid, lds, s);
+    } else {
+        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR, DRAIN>(a, grid, lds, s);
+        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR, DRAIN>(a, grid, lds, s);
+    }
+}
+// DRAIN variants (parked triangles prefetched) for launches that cannot fill the
+// chip (a.drained), one-lane-per-pixel ordered kernels only
 template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false, bool ENVIS = false>
 static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if (a.emit_inline) {
-        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR>(a, grid, lds, s);
-        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR>(a, grid, lds, s);
-    } else {
-        if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR>(a, grid, lds, s);
-        else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR>(a, grid, lds, s);
+    if constexpr (!PAIR && !ENVIS) {
+        if (a.drained) {
+            launch_ordered_d<LIGHTS, MTL_LDS, StackT, PAIR, ENVIS, true>(a, grid, lds, s);
+            return;
+        }
     }
+    launch_ordered_d<LIGHTS, MTL_LDS, StackT, PAIR, ENVIS, false>(a, grid, lds, s);
 }
 
 // LDS per 256-lane workgroup: [material table][traversal stack][path records],
