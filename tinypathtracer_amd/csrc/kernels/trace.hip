@@ -65,6 +65,10 @@
 // C3 4096 spp, 4 waves: +6.4 % (7,220 -> 7,685 Mrays/s, 2 interleaved reps)
 #define TPT_TRACE_WAVES_PAIR 4
 #endif
+#ifndef TPT_TRACE_WAVES_DRAIN
+// DRAIN variants (launches that cannot fill the chip: a few waves per SIMD anyway)
+#define TPT_TRACE_WAVES_DRAIN 4
+#endif
 #ifndef TPT_ENV_INLINE
 #define TPT_ENV_INLINE 0   // 1: env_lookup inlined in every variant (A/B builds)
 #endif
@@ -433,10 +437,44 @@ __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tr
 // of every passing leaf.  The closest hit under the ordered tie rule does not
 // depend on the order the leaves are tested in, so r ends as the traversal
 // would leave it.
+template <bool HOIST = false>
 __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restrict__ nd,
                                                   const float4* __restrict__ tri, int nint, uint32_t& c_leaf,
                                                   float cull_eps) {
     const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3], q4 = nd[4], q5 = nd[5], q6 = nd[6];
+    if constexpr (HOIST) {
+        // (DRAIN variants) the leaves' triangles are loaded together, before any
+        // test: the node's links are the same for every lane, so these are
+        // uniform loads issued at once instead of one round trip per leaf
+        float k0, k1, k2, k3, e0, e1, e2, e3;
+        slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
+        slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
+        slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
+        slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
+        const float hi = kRealMax, hd = 0.5f * kDelta;
+        const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
+                  i3 = __float_as_int(q6.w);
+        const int p0 = i0 >= 0 ? (i0 & kLinkMask) - nint : 0, p1 = i1 >= 0 ? (i1 & kLinkMask) - nint : 0,
+                  p2 = i2 >= 0 ? (i2 & kLinkMask) - nint : 0, p3 = i3 >= 0 ? (i3 & kLinkMask) - nint : 0;
+        const float4 a0 = tri[3 * p0], a1 = tri[3 * p0 + 1], a2 = tri[3 * p0 + 2];
+        const float4 b0 = tri[3 * p1], b1 = tri[3 * p1 + 1], b2 = tri[3 * p1 + 2];
+        float4 c0 = a0, c1 = a1, c2 = a2, d0 = a0, d1 = a1, d2 = a2;
+        if (i2 >= 0) {
+            c0 = tri[3 * p2];
+            c1 = tri[3 * p2 + 1];
+            c2 = tri[3 * p2 + 2];
+        }
+        if (i3 >= 0) {
+            d0 = tri[3 * p3];
+            d1 = tri[3 * p3 + 1];
+            d2 = tri[3 * p3 + 2];
+        }
+        if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test_q<true>(r, a0, a1, a2, p0, cull_eps); }
+        if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test_q<true>(r, b0, b1, b2, p1, cull_eps); }
+        if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test_q<true>(r, c0, c1, c2, p2, cull_eps); }
+        if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test_q<true>(r, d0, d1, d2, p3, cull_eps); }
+        return;
+    }
     float k0, k1, k2, k3, e0, e1, e2, e3;
     slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
@@ -836,7 +874,8 @@ struct PathRecords {
 // instead of 1 + lights, which is what bounds tail-heavy frames (C3).
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
           bool PAIR = false, bool DRAIN = false>
-__global__ __launch_bounds__(256, ENVIS ? TPT_TRACE_WAVES_IS : (PAIR ? TPT_TRACE_WAVES_PAIR : TPT_TRACE_WAVES))
+__global__ __launch_bounds__(256, ENVIS ? TPT_TRACE_WAVES_IS
+                                        : (PAIR ? TPT_TRACE_WAVES_PAIR : (DRAIN ? TPT_TRACE_WAVES_DRAIN : TPT_TRACE_WAVES)))
 void k_trace(TraceArgs a) {
     static_assert(!PAIR || (ORDERED && LIGHTS), "pair mode: ordered variants with 5-word records");
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1165,8 +1204,8 @@ void k_trace(TraceArgs a) {
                             phase = PH_PROBE;
                             if (r.mode == TM_EMIT && r.fin) {
                                 ++c_wide;
-                                emit_probe_inline(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf,
-                                                  a.cull_eps);
+                                emit_probe_inline<DRAIN>(r, a.inner4 + 8 * (size_t)a.emit_root, a.tri, nint, c_leaf,
+                                                         a.cull_eps);
                                 if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
                                 if (r.fid < 0) {
                                     ++c_local;
@@ -1209,7 +1248,47 @@ void k_trace(TraceArgs a) {
                 ts = TS_IDLE;
                 finish = false;
             }
-            if (finish) {   // unwind (:416-431): levels depth-1 .. 0
+            bool unwound = false;
+            if constexpr (DRAIN && !LIGHTS && MAXD == 8) {
+                // DRAIN variants: every level's record and materials read before the
+                // arithmetic, so the unwind pays one LDS latency chain instead of one
+                // per level (the same operations in the same order as below)
+                if (finish && rec.nlds >= 8) {
+                    unwound = true;
+                    float af[8];
+                    uint32_t w1[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        af[k] = rec.lds[(2 * k) * 256];
+                        w1[k] = k < depth ? __float_as_uint(rec.lds[(2 * k + 1) * 256]) : (kNoProbe << 15);
+                    }
+                    float4 mb[8];
+                    float ee[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        mb[k] = MT(2 * (w1[k] & 0x7fffu));
+                        const uint32_t pm = (w1[k] >> 15) & 0x7fffu;
+                        ee[k] = MT(2 * (pm == kNoProbe ? 0u : pm)).w;
+                    }
+#pragma unroll
+                    for (int k = 7; k >= 0; --k) {
+                        if (k < depth) {
+                            const V3 att = af[k] * v3(mb[k].x, mb[k].y, mb[k].z);   // :379
+                            const uint32_t kind = w1[k] >> 30;
+                            const float prob = kind == 0u ? af[k] : (kind == 1u ? -0.0f : 0.0f);
+                            const float ivp = 1.0f / prob;                            // :427 "/ pStack"
+                            const uint32_t pm = (w1[k] >> 15) & 0x7fffu;
+                            const float e = pm == kNoProbe ? 0.0f : ee[k];
+                            const V3 dst = pm == kNoProbe ? v3(0.0f, 0.0f, 0.0f)
+                                                          : (v3(1.0f, 1.0f, 1.0f) * v3(e, e, e)) + v3(0.0f, 0.0f, 0.0f);
+                            L = ivp * ((dst + L) * att);
+                        }
+                    }
+                    total = total + L;
+                    phase = PH_CAMERA;
+                }
+            }
+            if (finish && !unwound) {   // unwind (:416-431): levels depth-1 .. 0
                 for (int k = depth - 1; k >= 0; --k) {
                     const float af = rec.get(k, 0);
                     const uint32_t w1 = __float_as_uint(rec.get(k, 1));
