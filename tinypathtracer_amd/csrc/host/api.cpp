@@ -939,7 +939,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // half the path lanes and its heavy waves few traversing lanes, so it
     // batches less (C3 4096 spp: 4 -> 6.84, 2 -> 7.45, 8 -> 5.86 Grays/s;
     // C2, C4 and C5 within 2 % either way).
-    a.leaf_kb = p->leaf_batch > 0 ? std::min(p->leaf_batch, 64) : (pair_kernel ? 2 : 4);
+    // Drained launches likewise (strong-scaled C2, rank 0 of 8: 4 -> 259 ms, 2 -> 252 ms, 8 -> 277 ms).
+    a.leaf_kb = p->leaf_batch > 0 ? std::min(p->leaf_batch, 64) : ((pair_kernel || drained) ? 2 : 4);
     // XCD runs (trace.hip k_trace prologue) for scenes that do not fit one XCD's
     // 4 MiB L2 (≈ 200 B of nodes, triangles and shading data per face): the
     // largest run length <= 10 that divides a row's tiles per XCD (C5 3840 px:
