@@ -135,7 +135,8 @@ typedef struct {
                                         re-derived; the reference's trace never calls it, so the image
                                         differs from a reference render) */
 #define TPT_FLAG_APPROX_CULL   0x10  /* the ordered traversal's culls without the exactness guards (no
-                                        position slack, no sliver re-test): a few
+                                        position slack, no sliver re-test, grazing rays culled too;
+                                        DESIGN.md section 4): a few
                                         percent faster, and rays whose Moller-Trumbore t is rounding noise
                                         (sliver triangles, grazing edge hits) may then find another hit
                                         than the reference (5 of ~60 G rays over the BASELINE frames) */
@@ -238,12 +239,14 @@ tpt_status tpt_scene_read_world(tpt_scene* scene, float* wverts, float* wnorms);
  * each {v0..v4, d}. */
 tpt_status tpt_debug_rng_init(int device, uint64_t seed, uint64_t first_pixel, uint32_t n, uint32_t* states);
 /* Trace n rays (origins/dirs xyz) against the built BVH: hit fid (-1 miss), t, u, v.
+ * origin_fid: nullable; per ray the face it leaves (-1: none), for the render's
+ * grazing test (a ray within 1e-3 of that face's plane takes the uncull'd path).
  * mode 0: closest hit in the reference's visit order (traverseBVH, path_tracer.cu:61-107);
  * 1: closest hit through the render's traversal (nearer-first, culled, 4-wide);
  * 2: any hit (shadow rays); 3: the render's two-pass direct probe -- hit = the
  * closest hit if it is an emitter, -2 if a non-emitter is closer, -1 if no emitter is hit. */
 tpt_status tpt_debug_trace_rays(tpt_scene* scene, uint32_t n, const float* origins, const float* dirs,
-                                int32_t mode, int32_t* hit, float* t, float* uv);
+                                const int32_t* origin_fid, int32_t mode, int32_t* hit, float* t, float* uv);
 /* Known-answer evaluation of the trace kernel's own device functions, one case
  * per lane (tests pin them to the reference's headers):
  *   op 0 rayHitBBox   in 12/case (o3 d3 min3 max3)          out 2 (box_hit, min/max verdict)

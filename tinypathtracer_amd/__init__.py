@@ -218,16 +218,20 @@ class DeviceScene:
         check(lib().tpt_scene_read_world(self.handle, _ptr(wv), _ptr(wn)))
         return wv, wn
 
-    def trace_rays(self, origins, dirs, mode=0):
+    def trace_rays(self, origins, dirs, mode=0, origin_fid=None):
         """mode 0: the reference's visit order; 1: the render's ordered culled
-        traversal; 2: any hit; 3: two-pass probe (see tpt_debug_trace_rays)."""
+        traversal; 2: any hit; 3: two-pass probe (see tpt_debug_trace_rays).
+        origin_fid: per ray the face it leaves (-1 none), as the render knows it
+        for secondary rays (the grazing test)."""
         o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
         n = len(o)
         hit = np.zeros(n, np.int32)
         t = np.zeros(n, np.float32)
         uv = np.zeros((n, 2), np.float32)
-        check(lib().tpt_debug_trace_rays(self.handle, n, _ptr(o), _ptr(d), mode, _ptr(hit), _ptr(t), _ptr(uv)))
+        of = None if origin_fid is None else np.ascontiguousarray(origin_fid, np.int32).reshape(n)
+        check(lib().tpt_debug_trace_rays(self.handle, n, _ptr(o), _ptr(d), _ptr(of), mode, _ptr(hit), _ptr(t),
+                                         _ptr(uv)))
         return hit, t, uv
 
     def close(self):

@@ -96,8 +96,8 @@ SIGNATURES = [
     ("tpt_scene_read_bvh", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_scene_read_world", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_debug_rng_init", C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]),
-    ("tpt_debug_trace_rays", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
-                                       C.c_void_p, C.c_void_p]),
+    ("tpt_debug_trace_rays", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_debug_hot_kat", C.c_int, [C.c_int, C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("tpt_wide_tree_build", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                         C.POINTER(C.c_int32), C.c_int32]),

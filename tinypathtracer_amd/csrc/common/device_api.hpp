@@ -18,7 +18,8 @@
 //     even-depth nodes, each holding its up to 4 grandchildren (a leaf child
 //     stands for itself), bit 30 = emitter (ignored).
 //   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
-//   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, 0), (n2.xyz, 0)
+//   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, geometric normal: octahedral 2 x snorm16,
+//                      0x80008000 none), (n2.xyz, 0)
 //   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)
 #pragma once
 
@@ -94,6 +95,7 @@ struct TraceArgs {
     const float4* sliver_list;           // 2 per sliver: (exact leaf box lo.xyz, position | emissive << 30), (hi.xyz, 0)
     int32_t n_sliver_groups;             // 0: no sliver triangles
     float cull_eps;                      // absolute position slack of the t-culls (trace.hip "Culling")
+    int32_t graze;                       // 1: rays leaving a face within 1e-3 of its plane skip the culls (grazing())
     int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
     int32_t drained;                     // 1: the launch cannot fill the chip (latency-oriented DRAIN variants)
     int32_t xcd_run;                     // > 0: workgroup tiles dealt to XCDs in runs of this many (k_trace)
@@ -182,7 +184,7 @@ hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 // KAT kernel over the trace kernel's device functions (tpt_debug_hot_kat)
 hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipStream_t s);
-hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int mode, int32_t* hit,
-                             float* t, float* uv, hipStream_t s);
+hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, const int32_t* ofid,
+                             int mode, int32_t* hit, float* t, float* uv, hipStream_t s);
 
 }  // namespace tpt

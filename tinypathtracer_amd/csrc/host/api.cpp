@@ -799,6 +799,7 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.sliver_list = s->sliver_list.p;
     a.n_sliver_groups = s->n_sliver_groups;
     a.cull_eps = s->cull_eps;
+    a.graze = 1;
 #ifdef TPT_NO_EMIT_INLINE
     a.emit_inline = 0;   // A/B builds: probe pass 1 as a traversal always
 #else
@@ -898,6 +899,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     if (p->flags & TPT_FLAG_APPROX_CULL) {   // culls without the exactness guards (trace.hip "Culling")
         a.cull_eps = 0.0f;
         a.n_sliver_groups = 0;
+        a.graze = 0;
     }
     // A15 env next-event estimation: opt-in, needs an env with a non-empty distribution
     a.env_is = ((p->flags & TPT_FLAG_ENV_IS) && env && env->is_total > 0.0f) ? 1 : 0;
@@ -1238,22 +1240,28 @@ tpt_status tpt_debug_rng_init(int device, uint64_t seed, uint64_t first, uint32_
     return TPT_OK;
 }
 
-tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const float* d, int32_t mode, int32_t* hit,
-                                float* t, float* uv) {
+tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const float* d, const int32_t* origin_fid,
+                                int32_t mode, int32_t* hit, float* t, float* uv) {
     if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
     if (mode < 0 || mode > 3) return fail(TPT_ERR_INVALID_ARG, "unknown trace mode");
     if (n && (!o || !d || !hit || !t || !uv)) return fail(TPT_ERR_INVALID_ARG, "null argument");
     DeviceGuard g(s->device);
     DevBuf<float> dorg, ddir, dt, duv;
-    DevBuf<int32_t> dhit;
+    DevBuf<int32_t> dhit, dofid;
     HIP_OR_FAIL(dorg.upload(o, 3 * (size_t)n, s->stream));
+    if (origin_fid) {
+        for (uint32_t i = 0; i < n; ++i)
+            if (origin_fid[i] >= s->n_faces) return fail(TPT_ERR_INVALID_ARG, "origin face out of range");
+        HIP_OR_FAIL(dofid.upload(origin_fid, n, s->stream));
+    }
     HIP_OR_FAIL(ddir.upload(d, 3 * (size_t)n, s->stream));
     HIP_OR_FAIL(dhit.alloc(n));
     HIP_OR_FAIL(dt.alloc(n));
     HIP_OR_FAIL(duv.alloc(2 * (size_t)n));
     tpt::TraceArgs a{};
     fill_trace_args(s, nullptr, nullptr, a);
-    HIP_OR_FAIL(tpt::launch_trace_rays(a, n, dorg.p, ddir.p, mode, dhit.p, dt.p, duv.p, s->stream));
+    HIP_OR_FAIL(tpt::launch_trace_rays(a, n, dorg.p, ddir.p, origin_fid ? dofid.p : nullptr, mode, dhit.p, dt.p, duv.p,
+                                       s->stream));
     HIP_OR_FAIL(hipStreamSynchronize(s->stream));
     if (n) {
         HIP_OR_FAIL(hipMemcpy(hit, dhit.p, 4 * (size_t)n, hipMemcpyDeviceToHost));

@@ -188,7 +188,7 @@ struct Trav {
 };
 
 __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool boxes_finite = false,
-                                           int emit_root = -1, float cull_eps = 0.0f) {
+                                           int emit_root = -1, float cull_eps = 0.0f, bool graze = false) {
     r.o = o;
     r.d = d;
     r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
@@ -201,7 +201,9 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
     r.u = 0.0f;
     r.v = 0.0f;
     r.mode = mode;
-    r.fin = boxes_finite & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
+    // (graze: a ray leaving a surface within 1e-3 of its plane takes the uncull'd
+    // binary path, "Culling" above)
+    r.fin = boxes_finite & !graze & __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
             __builtin_isfinite(r.inv.x) & __builtin_isfinite(r.inv.y) & __builtin_isfinite(r.inv.z);
     r.lim = kRealMax;   // t = FLT_MAX: nothing to cull against yet
     (void)cull_eps;
@@ -212,6 +214,32 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
         if (emit_root >= 0) r.node = emit_root;
         else r.mode = TM_CLOSEST;
     }
+}
+
+// Rays leaving a surface almost in its plane (Culling, "rays grazing a
+// triangle's plane"): |cos(d, n)| < kGraze against the geometric normal of the
+// face the ray leaves (shade record, octahedral snorm16).  Adversarial rays that
+// the culled walk resolves differently from the reference all leave their face
+// at sin < 1e-4 (origins on its vertices and edges; tools/cull_diag.py); such
+// rays take the binary path, which tests every leaf whose box the line passes
+// (no culls), so they find the reference's hit.  0x80008000: no surface (camera
+// rays, degenerate faces).
+constexpr float kGraze = 1e-3f;
+constexpr uint32_t kNoSurface = 0x80008000u;
+__device__ __forceinline__ bool grazing(uint32_t gn, V3 d) {
+    if (gn == kNoSurface) return false;
+    float u = (float)(int)(int16_t)(gn & 0xffffu) * (1.0f / 32767.0f);
+    float v = (float)(int)(int16_t)(gn >> 16) * (1.0f / 32767.0f);
+    const float z = 1.0f - fabsf(u) - fabsf(v);
+    if (z < 0.0f) {
+        const float tu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
+        const float tv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
+        u = tu;
+        v = tv;
+    }
+    const float dn = d.x * u + d.y * v + d.z * z;
+    const float nn = u * u + v * v + z * z, dd = d.x * d.x + d.y * d.y + d.z * d.z;
+    return dn * dn < (kGraze * kGraze) * nn * dd;
 }
 
 // Visit of inner node r.node: the child to descend into (-1: none) and, when
@@ -979,6 +1007,11 @@ void k_trace(TraceArgs a) {
     bool vpend = false;   // a traversal of this lane awaits verification
 #endif
     bool sl_pend = false;   // a traversal of this lane awaits the sliver pass
+    // grazing() inputs: LIGHTS variants keep the geometric normal of the face the
+    // current rays leave (shadow rays start in later passes); the others only the
+    // verdict for the next extension ray
+    uint32_t gsurf = kNoSurface;
+    bool graze_next = false;
     // DRAIN variants (launches too small to fill the chip, where each wave's
     // chain latency is the frame time): a parked leaf's triangle is loaded when
     // the leaf is parked, in flight while the walk goes on (strong-scaled C2,
@@ -1078,6 +1111,7 @@ void k_trace(TraceArgs a) {
             bool begun = false;   // the next ray is already set up (inline probe pass 1)
             V3 L = v3(0.0f, 0.0f, 0.0f);
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
+            uint32_t gpass = gsurf;   // the face this pass's new rays leave
             if (phase == PH_EXT) {
                 if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
                     if (a.env) L = env_lookup<ENVIS>(a.env, a.env_w, a.env_h, rd);
@@ -1089,11 +1123,14 @@ void k_trace(TraceArgs a) {
                     const float w = 1.0f - r.u - r.v;
                     nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (r.u * v3(s1.x, s1.y, s1.z))) +
                                     (r.v * v3(s2.x, s2.y, s2.z)));
+                    gpass = a.graze ? __float_as_uint(s1.w) : kNoSurface;
+                    if constexpr (LIGHTS) gsurf = gpass;
                     r.o = r.o + (r.t * rd);
                     const int mtl = __float_as_int(s0.w);
                     const float4 m1 = MT(2 * mtl + 1);
                     float af;
                     const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
+                    graze_next = grazing(gpass, nd);
                     rec.put(depth, 0, af);
                     mk = (uint32_t)mtl | (p_kind(prob) << 30);
                     direct = v3(0.0f, 0.0f, 0.0f);
@@ -1131,6 +1168,7 @@ void k_trace(TraceArgs a) {
             TPT_SEC(1)
             V3 td = rd;
             bool shadow = false;
+            bool tg = false;   // the next ray leaves its face within 1e-3 of its plane (grazing())
             if (PAIR && lights_next && !side && li == 0 && pend < 0 && (a.n_lights > 0 || (ENVIS && env_pending))) {
                 // hand this bounce's shadow rays to the idle side lane (posted at the
                 // exchange below: origin r.o, material mk, level depth)
@@ -1161,6 +1199,7 @@ void k_trace(TraceArgs a) {
                 if (LIGHTS && li < a.n_lights) {
                     V3 lrad;
                     light_sample(a.lights, li, r.o, td, lrad);
+                    tg = grazing(gsurf, td);
                     phase = PH_SHADOW;
                     shadow = true;
                 } else {
@@ -1178,6 +1217,7 @@ void k_trace(TraceArgs a) {
                             phase = PH_ENVSHADOW;
                             shadow = true;
                             env_ray = true;
+                            tg = grazing(gsurf, td);
                         }
                     }
                     if (env_ray) {
@@ -1187,6 +1227,7 @@ void k_trace(TraceArgs a) {
                     } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
                         float af2;
                         new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
+                        tg = grazing(gpass, td);
                         if (TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) {
                             // no triangle emits: the probe's emitter pass ends at the
                             // root with no hit, exactly as a traversal would (the ray
@@ -1199,7 +1240,7 @@ void k_trace(TraceArgs a) {
                             // <= 4 emitters: pass 1 here; a miss resolves the probe in
                             // this pass, an emitter hit goes on to pass 2 (occlusion)
                             ++c_trav;
-                            trav_begin(r, r.o, td, TM_EMIT, a.boxes_finite != 0, a.emit_root, a.cull_eps);
+                            trav_begin(r, r.o, td, TM_EMIT, a.boxes_finite != 0, a.emit_root, a.cull_eps, tg);
                             begun = true;
                             phase = PH_PROBE;
                             if (r.mode == TM_EMIT && r.fin) {
@@ -1235,6 +1276,7 @@ void k_trace(TraceArgs a) {
                 } else {
                     rd = nd;
                     td = rd;
+                    tg = graze_next;
                     ++depth;
                     if (depth == a.max_depth) finish = true;
                     else phase = PH_EXT;
@@ -1339,6 +1381,7 @@ void k_trace(TraceArgs a) {
                     rd = normalize(v3(r4[0], r4[1], r4[2]));
                     td = rd;
                     to = v3(a.origin[0], a.origin[1], a.origin[2]);
+                    tg = false;   // the camera: no surface
                     depth = 0;
                     phase = PH_EXT;
                 }
@@ -1348,7 +1391,7 @@ void k_trace(TraceArgs a) {
                 if (!begun) {
                     ++c_trav;
                     trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
-                               a.boxes_finite != 0, a.emit_root, a.cull_eps);
+                               a.boxes_finite != 0, a.emit_root, a.cull_eps, tg);
                 }
                 ts = TS_TRAV;
                 sl_pend = true;
@@ -1365,6 +1408,7 @@ void k_trace(TraceArgs a) {
             const int jpost = __shfl_xor((int)post, 1, 64);
             const float jx = __shfl_xor(r.o.x, 1, 64), jy = __shfl_xor(r.o.y, 1, 64), jz = __shfl_xor(r.o.z, 1, 64);
             const int jmk = __shfl_xor((int)mk, 1, 64), jl = __shfl_xor(jlevel, 1, 64);
+            const uint32_t jgs = (uint32_t)__shfl_xor((int)gsurf, 1, 64);
             bool jenv = false;
             if constexpr (ENVIS) {   // A15: the env sample's uniforms and normal travel with the job
                 jenv = __shfl_xor((int)post_env, 1, 64) != 0;
@@ -1381,6 +1425,7 @@ void k_trace(TraceArgs a) {
             if (side && jpost) {
                 mk = (uint32_t)jmk;
                 jlevel = jl;
+                gsurf = jgs;
                 li = 0;
                 direct = v3(0.0f, 0.0f, 0.0f);
                 V3 ldir, lrad;
@@ -1398,7 +1443,7 @@ void k_trace(TraceArgs a) {
                 }
                 if (go) {
                     ++c_trav;
-                    trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root, a.cull_eps);
+                    trav_begin(r, jo, ldir, TM_ANY, a.boxes_finite != 0, a.emit_root, a.cull_eps, grazing(gsurf, ldir));
                     ts = TS_TRAV;
                     sl_pend = true;
 #ifdef TPT_VERIFY_CULL
@@ -1637,8 +1682,8 @@ __device__ __forceinline__ void trav_lane(Trav& r, const TraceArgs& a, LaneStack
 }
 
 __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, const float* __restrict__ o,
-                                                    const float* __restrict__ d, int mode, int32_t* hit, float* t,
-                                                    float* uv) {
+                                                    const float* __restrict__ d, const int32_t* __restrict__ ofid,
+                                                    int mode, int32_t* hit, float* t, float* uv) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     uint32_t c_ovf = 0;
@@ -1655,7 +1700,10 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
             fid = r.fid;
         } else {
             const int tm = mode == 1 ? TM_CLOSEST : (mode == 2 ? TM_ANY : TM_EMIT);
-            trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root, a.cull_eps);
+            // a ray leaving face ofid[i] (>= 0) gets the render's grazing test
+            const uint32_t gs =
+                (a.graze && ofid && ofid[i] >= 0) ? __float_as_uint(a.shade[3 * ofid[i] + 1].w) : kNoSurface;
+            trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root, a.cull_eps, grazing(gs, rdir));
             uint32_t c_leaf = 0;
             trav_lane<true>(r, a, stk, c_ovf);
             if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
@@ -1906,11 +1954,11 @@ hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, int mode, int32_t* hit,
-                             float* t, float* uv, hipStream_t s) {
+hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, const float* d, const int32_t* ofid,
+                             int mode, int32_t* hit, float* t, float* uv, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t lds = (size_t)kRaysLdsSlots * 256 * sizeof(int);
-    hipLaunchKernelGGL(k_trace_rays, dim3((n + 255) / 256), dim3(256), lds, s, a, n, o, d, mode, hit, t, uv);
+    hipLaunchKernelGGL(k_trace_rays, dim3((n + 255) / 256), dim3(256), lds, s, a, n, o, d, ofid, mode, hit, t, uv);
     return hipGetLastError();
 }
 
