@@ -292,31 +292,25 @@ __global__ void k_pack_shade(BuildBuffers b) {
     int mtl = b.lut[find_object(f, b.lut, b.n_objects)].y;
     if (mtl < 0 || mtl >= b.n_materials) mtl = b.n_materials;   // -> Material() slot (App. A.9)
     float4* s = b.shade + 3 * f;
-    // the face's geometric unit normal, octahedral 2 x snorm16 (error < 1e-4): the
-    // trace kernel's grazing test for rays leaving this face (trace.hip "Culling")
+    // the face's geometric unit normal n for the trace kernel's grazing test of rays
+    // leaving this face (trace.hip grazing(), "Culling"): n.x in s[1].w, n.y in
+    // s[2].w, the sign of n.z in n.x's lowest mantissa bit (1: negative); n.z is
+    // recomputed from the unit length.  A non-finite n.x marks "no normal"
+    // (degenerate or non-finite face: never grazing).
     const float* v = b.wverts;
     const float ax = v[3 * i1] - v[3 * i0], ay = v[3 * i1 + 1] - v[3 * i0 + 1], az = v[3 * i1 + 2] - v[3 * i0 + 2];
     const float bx = v[3 * i2] - v[3 * i0], by = v[3 * i2 + 1] - v[3 * i0 + 1], bz = v[3 * i2 + 2] - v[3 * i0 + 2];
-    float gx = ay * bz - az * by, gy = az * bx - ax * bz, gz = ax * by - ay * bx;
-    const float l1 = fabsf(gx) + fabsf(gy) + fabsf(gz);
-    uint32_t gn = 0x80008000u;   // no normal (degenerate or non-finite face; not an encoding): never grazing
-    if (l1 > 0.0f && __builtin_isfinite(l1)) {
-        gx /= l1;
-        gy /= l1;
-        gz /= l1;
-        if (gz < 0.0f) {
-            const float tx = (1.0f - fabsf(gy)) * (gx < 0.0f ? -1.0f : 1.0f);
-            const float ty = (1.0f - fabsf(gx)) * (gy < 0.0f ? -1.0f : 1.0f);
-            gx = tx;
-            gy = ty;
-        }
-        const int qx = (int)rintf(fminf(fmaxf(gx, -1.0f), 1.0f) * 32767.0f);
-        const int qy = (int)rintf(fminf(fmaxf(gy, -1.0f), 1.0f) * 32767.0f);
-        gn = ((uint32_t)qx & 0xffffu) | ((uint32_t)qy << 16);
+    const float gx = ay * bz - az * by, gy = az * bx - ax * bz, gz = ax * by - ay * bx;
+    const float len = sqrtf(gx * gx + gy * gy + gz * gz);
+    float nxs = __builtin_nanf(""), nys = 0.0f;
+    if (len > 0.0f && __builtin_isfinite(len)) {
+        const uint32_t xb = (__float_as_uint(gx / len) & ~1u) | (gz < 0.0f ? 1u : 0u);
+        nxs = __uint_as_float(xb);
+        nys = gy / len;
     }
     s[0] = make_float4(w[3 * i0], w[3 * i0 + 1], w[3 * i0 + 2], __int_as_float(mtl));
-    s[1] = make_float4(w[3 * i1], w[3 * i1 + 1], w[3 * i1 + 2], __uint_as_float(gn));
-    s[2] = make_float4(w[3 * i2], w[3 * i2 + 1], w[3 * i2 + 2], 0.0f);
+    s[1] = make_float4(w[3 * i1], w[3 * i1 + 1], w[3 * i1 + 2], nxs);
+    s[2] = make_float4(w[3 * i2], w[3 * i2 + 1], w[3 * i2 + 2], nys);
 }
 
 // Reference node layout (bvh.cuh:52-58) for introspection / parity tests.

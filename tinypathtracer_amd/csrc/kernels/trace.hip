@@ -217,29 +217,26 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
 }
 
 // Rays leaving a surface almost in its plane (Culling, "rays grazing a
-// triangle's plane"): |cos(d, n)| < kGraze against the geometric normal of the
-// face the ray leaves (shade record, octahedral snorm16).  Adversarial rays that
-// the culled walk resolves differently from the reference all leave their face
-// at sin < 1e-4 (origins on its vertices and edges; tools/cull_diag.py); such
-// rays take the binary path, which tests every leaf whose box the line passes
-// (no culls), so they find the reference's hit.  0x80008000: no surface (camera
+// triangle's plane"): |cos(d, n)| < kGraze against the geometric unit normal of
+// the face the ray leaves (shade record: n.x, n.y, the sign of n.z in n.x's
+// lowest bit).  Adversarial rays that the culled walk resolves differently from
+// the reference all leave their face at sin < 1e-4 (origins on its vertices and
+// edges; tools/cull_diag.py); such rays take the binary path, which tests every
+// leaf whose box the line passes (no culls), so they find the reference's hit.
+// A face is carried as the pair (n.x bits, n.y); NaN n.x: no surface (camera
 // rays, degenerate faces).
 constexpr float kGraze = 1e-3f;
-constexpr uint32_t kNoSurface = 0x80008000u;
-__device__ __forceinline__ bool grazing(uint32_t gn, V3 d) {
-    if (gn == kNoSurface) return false;
-    float u = (float)(int)(int16_t)(gn & 0xffffu) * (1.0f / 32767.0f);
-    float v = (float)(int)(int16_t)(gn >> 16) * (1.0f / 32767.0f);
-    const float z = 1.0f - fabsf(u) - fabsf(v);
-    if (z < 0.0f) {
-        const float tu = (1.0f - fabsf(v)) * (u < 0.0f ? -1.0f : 1.0f);
-        const float tv = (1.0f - fabsf(u)) * (v < 0.0f ? -1.0f : 1.0f);
-        u = tu;
-        v = tv;
-    }
-    const float dn = d.x * u + d.y * v + d.z * z;
-    const float nn = u * u + v * v + z * z, dd = d.x * d.x + d.y * d.y + d.z * d.z;
-    return dn * dn < (kGraze * kGraze) * nn * dd;
+struct Surf {
+    float x, y;
+};
+__device__ __forceinline__ Surf no_surface() { return Surf{__builtin_nanf(""), 0.0f}; }
+__device__ __forceinline__ bool grazing(Surf g, V3 d) {
+    if (!(g.x == g.x)) return false;
+    const float zz = fmaxf(0.0f, 1.0f - g.x * g.x - g.y * g.y);
+    const float z = (__float_as_uint(g.x) & 1u) ? -__builtin_amdgcn_sqrtf(zz) : __builtin_amdgcn_sqrtf(zz);
+    const float dn = d.x * g.x + d.y * g.y + d.z * z;
+    const float dd = d.x * d.x + d.y * d.y + d.z * d.z;
+    return dn * dn < (kGraze * kGraze) * dd;   // (|n| = 1 to ~1e-7)
 }
 
 // Visit of inner node r.node: the child to descend into (-1: none) and, when
@@ -1010,7 +1007,7 @@ void k_trace(TraceArgs a) {
     // grazing() inputs: LIGHTS variants keep the geometric normal of the face the
     // current rays leave (shadow rays start in later passes); the others only the
     // verdict for the next extension ray
-    uint32_t gsurf = kNoSurface;
+    Surf gsurf = no_surface();
     bool graze_next = false;
     // DRAIN variants (launches too small to fill the chip, where each wave's
     // chain latency is the frame time): a parked leaf's triangle is loaded when
@@ -1111,7 +1108,7 @@ void k_trace(TraceArgs a) {
             bool begun = false;   // the next ray is already set up (inline probe pass 1)
             V3 L = v3(0.0f, 0.0f, 0.0f);
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
-            uint32_t gpass = gsurf;   // the face this pass's new rays leave
+            Surf gpass = gsurf;   // the face this pass's new rays leave
             if (phase == PH_EXT) {
                 if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
                     if (a.env) L = env_lookup<ENVIS>(a.env, a.env_w, a.env_h, rd);
@@ -1123,7 +1120,7 @@ void k_trace(TraceArgs a) {
                     const float w = 1.0f - r.u - r.v;
                     nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (r.u * v3(s1.x, s1.y, s1.z))) +
                                     (r.v * v3(s2.x, s2.y, s2.z)));
-                    gpass = a.graze ? __float_as_uint(s1.w) : kNoSurface;
+                    gpass = a.graze ? Surf{s1.w, s2.w} : no_surface();
                     if constexpr (LIGHTS) gsurf = gpass;
                     r.o = r.o + (r.t * rd);
                     const int mtl = __float_as_int(s0.w);
@@ -1408,7 +1405,7 @@ void k_trace(TraceArgs a) {
             const int jpost = __shfl_xor((int)post, 1, 64);
             const float jx = __shfl_xor(r.o.x, 1, 64), jy = __shfl_xor(r.o.y, 1, 64), jz = __shfl_xor(r.o.z, 1, 64);
             const int jmk = __shfl_xor((int)mk, 1, 64), jl = __shfl_xor(jlevel, 1, 64);
-            const uint32_t jgs = (uint32_t)__shfl_xor((int)gsurf, 1, 64);
+            const Surf jgs = Surf{__shfl_xor(gsurf.x, 1, 64), __shfl_xor(gsurf.y, 1, 64)};
             bool jenv = false;
             if constexpr (ENVIS) {   // A15: the env sample's uniforms and normal travel with the job
                 jenv = __shfl_xor((int)post_env, 1, 64) != 0;
@@ -1701,8 +1698,9 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
         } else {
             const int tm = mode == 1 ? TM_CLOSEST : (mode == 2 ? TM_ANY : TM_EMIT);
             // a ray leaving face ofid[i] (>= 0) gets the render's grazing test
-            const uint32_t gs =
-                (a.graze && ofid && ofid[i] >= 0) ? __float_as_uint(a.shade[3 * ofid[i] + 1].w) : kNoSurface;
+            const Surf gs = (a.graze && ofid && ofid[i] >= 0)
+                                ? Surf{a.shade[3 * ofid[i] + 1].w, a.shade[3 * ofid[i] + 2].w}
+                                : no_surface();
             trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root, a.cull_eps, grazing(gs, rdir));
             uint32_t c_leaf = 0;
             trav_lane<true>(r, a, stk, c_ovf);
