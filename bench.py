@@ -87,6 +87,10 @@ def parse():
     ap.add_argument("--build-threads", type=int, default=-2,
                     help="host threads of the traversal-tree build (tpt_scene_set_build_threads); "
                          "-2: this process's share of the usable cores (cores / local ranks)")
+    ap.add_argument("--async-build", type=int, default=1,
+                    help="1: the per-frame scene build's host SAH trees finish on a background thread while the "
+                         "render enqueues its RNG initialisation (tpt_scene_build_async); the render's wait for "
+                         "them is phase 'tree_wait'. 0: tpt_scene_build (all of it in 'scene_build')")
     ap.add_argument("--env", choices=["sky", "none"], default=None, help="procedural equirect env on miss")
     ap.add_argument("--env-is", action="store_true",
                     help="opt-in env next-event estimation with importance sampling (A15; changes the image)")
@@ -313,7 +317,7 @@ def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_lau
 
 
 KEYS = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
-        "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms", "local_rays"]
+        "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms", "local_rays", "tree_wait_ms"]
 
 
 def main():
@@ -381,7 +385,7 @@ def main():
         def step():
             # doTrace rebuilds the world transform and the BVH every frame (path_tracer.cu:536-542)
             tb = time.perf_counter()
-            d_scene.build()
+            d_scene.build(asynchronous=bool(args.async_build))
             build_ms.append((time.perf_counter() - tb) * 1e3)
             st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
                                   radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
@@ -516,10 +520,12 @@ def main():
                                for k in ("wide_visits", "internal_visits", "leaf_tests")},
             "roofline": roof,
             "phases_ms_per_step": {"scene_build": round(sum(build_ms) / K, 3),
+                                   "tree_wait": round(l_tot["tree_wait_ms"] / K, 3),
                                    "rng_init": round(l_tot["rng_init_ms"] / K, 3),
                                    "trace": round(l_tot["trace_ms"] / K, 3),
                                    "resolve": round(l_tot["resolve_ms"] / K, 3)},
             "build_threads": build_threads,
+            "async_build": int(args.async_build),
         }
         if per_rank_ms:
             out["per_rank_ms"] = per_rank_ms

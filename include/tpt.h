@@ -164,6 +164,8 @@ typedef struct {
     uint64_t local_rays;          /* of `traversals`, the direct probes resolved in the shading pass without
                                      a BVH traversal (no emissive triangle, or a miss of the <= 4-emitter
                                      inline test); traversals - local_rays = BVH traversals run */
+    double tree_wait_ms;          /* host wall time this call waited for a tpt_scene_build_async's host
+                                     traversal-tree build, after enqueueing the RNG initialisation */
 } tpt_stats;
 
 typedef struct tpt_scene tpt_scene;
@@ -180,6 +182,15 @@ tpt_status tpt_scene_create(const tpt_scene_desc* desc, int device, tpt_scene** 
 /* World transform + LBVH build on the device (path_tracer.cu:536-542,
  * bvh.cu:304-331) and the packed traversal layout. */
 tpt_status tpt_scene_build(tpt_scene* scene);
+/* tpt_scene_build whose host half -- the SAH traversal trees over the LBVH's
+ * leaf boxes -- continues on a host thread after the call returns (the device
+ * LBVH build and its read-back are done).  The next call that traces the scene
+ * waits for it: tpt_render / tpt_render_frames after enqueueing the per-pixel
+ * RNG initialisation (setupRandSeed, path_tracer.cu:513), so the two overlap;
+ * tpt_debug_trace_rays first.  A failure of the host half is reported by that
+ * call.  tpt_scene_build / _async and tpt_scene_destroy supersede a pending
+ * one.  The scene is the same as tpt_scene_build's. */
+tpt_status tpt_scene_build_async(tpt_scene* scene);
 /* Host threads of the traversal-tree build inside tpt_scene_build (the SAH
  * 4-wide tree): < 0 = auto (the cores this process may
  * use: its affinity mask capped by the cgroup CPU quota), 0 or 1 = serial.

@@ -38,7 +38,7 @@ static int check_wide(int n, unsigned seed) {
     }
     std::vector<int> pos((size_t)n);
     for (int i = 0; i < n; ++i) pos[i] = i;
-    std::vector<float> out;
+    tpt::HostFloats out;
     int need = 0;
     tpt::WideParams prm;
     const int nodes = tpt::build_wide_sah(pos, box.data(), emit.data(), n - 1, 0, out, &need, prm);

@@ -198,9 +198,12 @@ class DeviceScene:
         check(lib().tpt_scene_set_build_threads(self.handle, int(threads)))
         return self
 
-    def build(self):
-        """World transform + LBVH (path_tracer.cu:536-542) on the device."""
-        check(lib().tpt_scene_build(self.handle))
+    def build(self, asynchronous: bool = False):
+        """World transform + LBVH (path_tracer.cu:536-542) on the device, then
+        the host SAH traversal trees.  asynchronous=True: the host trees finish
+        on a background thread (tpt_scene_build_async) while the next render
+        enqueues its RNG initialisation; that render waits for them."""
+        check(lib().tpt_scene_build_async(self.handle) if asynchronous else lib().tpt_scene_build(self.handle))
         self.built = True
         return self
 

@@ -67,7 +67,7 @@ class Stats(C.Structure):
                 ("rng_init_ms", C.c_double), ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("total_ms", C.c_double), ("trace_launches", C.c_int32), ("pad", C.c_int32),
                 ("wide_visits", C.c_uint64), ("accumulated_spp", C.c_uint64), ("trace_kernel_ms", C.c_double),
-                ("local_rays", C.c_uint64)]
+                ("local_rays", C.c_uint64), ("tree_wait_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
@@ -80,6 +80,7 @@ SIGNATURES = [
     ("tpt_device_count", C.c_int, []),
     ("tpt_scene_create", C.c_int, [C.POINTER(SceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     ("tpt_scene_build", C.c_int, [C.c_void_p]),
+    ("tpt_scene_build_async", C.c_int, [C.c_void_p]),
     ("tpt_scene_set_build_threads", C.c_int, [C.c_void_p, C.c_int32]),
     ("tpt_scene_destroy", None, [C.c_void_p]),
     ("tpt_env_create", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int, C.POINTER(C.c_void_p)]),

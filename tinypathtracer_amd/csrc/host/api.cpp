@@ -12,8 +12,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
+#include <system_error>
+#include <thread>
 #include <vector>
 
 #include "../common/device_api.hpp"
@@ -197,6 +200,85 @@ int pow2_at_least(int n) {
 
 }  // namespace
 
+namespace {
+// TPT_BUILD_TIMING=1: per-phase wall times of tpt_scene_build on stderr
+struct PhaseClock {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    explicit PhaseClock(bool on_) : on(on_), t(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "tpt_scene_build %-10s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
+
+// The host half of a scene build: the SAH traversal trees over the LBVH's leaf
+// boxes (wide_bvh.cpp).  Pure host work on its own copies -- no HIP call, no
+// access to the scene -- so tpt_scene_build_async runs it on a thread of its
+// own while the caller goes on (tpt_render enqueues the RNG initialisation,
+// then waits for it: finish_pending).
+struct HostTrees {
+    size_t n = 0;
+    std::vector<float> lbox;
+    std::vector<uint32_t> lemit;
+    tpt::WideParams prm;
+    int32_t lbvh_n4 = 0;      // the LBVH even-depth view's node count (inner4 when no SAH tree)
+    bool timing = false;
+    // results
+    tpt::HostFloats w4, e4;
+    int n4 = -1, need = 0, ne4 = -1, eneed = 0;
+    tpt_status st = TPT_OK;
+    std::string msg;
+    std::thread th;
+    ~HostTrees() {
+        if (th.joinable()) th.join();
+    }
+    bool main_ok() const { return n4 > 0 && (size_t)n4 <= n - 1 && need <= 150; }
+    int32_t base() const { return main_ok() ? n4 : lbvh_n4; }   // the emitter tree's first id
+    bool emit_ok() const { return ne4 > 0 && (size_t)(base() + ne4) <= n - 1 && eneed <= 150; }
+};
+
+void build_host_trees(HostTrees& j) {
+    PhaseClock clk(j.timing);
+    const size_t n = j.n;
+    const int leaf_base = (int)n - 1;
+#ifdef TPT_WIDE_TREE_LBVH
+    const bool sah = false;   // A/B builds: keep the LBVH's even-depth view
+#else
+    const bool sah = true;
+#endif
+    try {
+        if (sah) {
+            // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
+            std::vector<int> all(n);
+            for (size_t p = 0; p < n; ++p) all[p] = (int)p;
+            j.n4 = tpt::build_wide_sah(all, j.lbox.data(), j.lemit.data(), leaf_base, 0, j.w4, &j.need, j.prm);
+        }
+        clk.mark("sah");
+        // The direct probe's first pass (closest emissive hit, trace.hip
+        // TM_EMIT) walks a tree over the emissive triangles alone, appended
+        // after the main tree's nodes: same exact leaf boxes and positions, so
+        // the same hit as the emitter-filtered walk of the whole tree.
+        std::vector<int> em;
+        for (size_t p = 0; p < n; ++p)
+            if (j.lemit[p]) em.push_back((int)p);
+        if (!em.empty())
+            j.ne4 = tpt::build_wide_sah(em, j.lbox.data(), j.lemit.data(), leaf_base, j.base(), j.e4, &j.eneed, j.prm);
+        clk.mark("emit_tree");
+    } catch (const std::bad_alloc&) {
+        j.st = TPT_ERR_OOM;
+        j.msg = "traversal tree build: host allocation failed";
+    } catch (const std::exception& ex) {
+        j.st = TPT_ERR_HIP;
+        j.msg = std::string("traversal tree build: ") + ex.what();
+    }
+}
+
+}  // namespace
+
 struct tpt_scene {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -216,6 +298,8 @@ struct tpt_scene {
     float cull_eps = 0.0f;                  // absolute position slack of the t-culls
     uint32_t tree_depth = 0;
     int32_t build_threads = -1;             // SAH tree build threads (tpt_scene_set_build_threads)
+    std::unique_ptr<HostTrees> pending;     // tpt_scene_build_async's host half, until finish_pending
+    uint32_t pending_need = 0;              // its stack bound before the trees
     // inputs
     DevBuf<uint32_t> indices;
     DevBuf<float> vertices, normals, vert_trans, normal_trans;
@@ -439,8 +523,61 @@ tpt_status tpt_scene_set_build_threads(tpt_scene* s, int32_t threads) {
     return TPT_OK;
 }
 
-tpt_status tpt_scene_build(tpt_scene* s) {
+namespace {
+
+// Uploads a finished HostTrees job and completes the scene (the stack bound).
+tpt_status upload_host_trees(tpt_scene* s, HostTrees& j, uint32_t* wide_need) {
+    if (j.st != TPT_OK) return fail(j.st, j.msg);
+    if (j.main_ok()) {
+        HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, j.w4.data(), j.w4.size() * sizeof(float), hipMemcpyHostToDevice,
+                                   s->stream));
+        s->n4 = j.n4;
+        *wide_need = (uint32_t)j.need;
+        s->wide_tree = 1;
+    }
+    if (j.emit_ok()) {
+        HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p + 8 * (size_t)s->n4, j.e4.data(), j.e4.size() * sizeof(float),
+                                   hipMemcpyHostToDevice, s->stream));
+        s->emit_root = s->n4;
+        s->emit_inline = j.ne4 == 1 ? 1 : 0;
+        *wide_need = std::max(*wide_need, (uint32_t)j.eneed);
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(s->stream));   // (the host buffers are freed after this)
+    return TPT_OK;
+}
+
+// Stack capacity: the binary DFS that pushes one sibling per level holds at
+// most depth + 1 entries; the 4-wide ordered walk holds at most the tree's
+// stack need (wide_bvh.cpp), 3 * ceil(depth / 2) for the LBVH's even-depth view.
+tpt_status finish_stack(tpt_scene* s, uint32_t wide_need) {
+    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(s->tree_depth + 2, wide_need), 2);
+    if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
+    s->built = true;
+    return TPT_OK;
+}
+
+}  // namespace
+
+// Joins an asynchronous build's host half and uploads its trees (a no-op
+// without one).  Every entry point that reads the traversal trees calls it.
+static tpt_status finish_pending(tpt_scene* s, double* wait_ms = nullptr) {
+    if (!s->pending) return TPT_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::unique_ptr<HostTrees> j = std::move(s->pending);
+    if (j->th.joinable()) j->th.join();
+    if (wait_ms) *wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    DeviceGuard g(s->device);
+    uint32_t wide_need = s->pending_need;
+    tpt_status st = upload_host_trees(s, *j, &wide_need);
+    if (st == TPT_OK) st = finish_stack(s, wide_need);
+    if (st != TPT_OK) s->built = false;
+    return st;
+}
+
+static tpt_status scene_build(tpt_scene* s, bool async) {
     if (!s) return fail(TPT_ERR_INVALID_ARG, "null scene");
+    s->pending.reset();   // a previous asynchronous build still running: its trees are superseded
+    s->built = false;
     DeviceGuard g(s->device);
     const size_t n = (size_t)s->n_faces, nn = 2 * n - 1, nv = (size_t)s->n_vertices;
     size_t sort_bytes = 0;
@@ -472,6 +609,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
     HIP_OR_FAIL(s->shade.alloc(3 * n));
     HIP_OR_FAIL(s->nodes36.alloc(36 * nn));
     HIP_OR_FAIL(hipMemsetAsync(s->parent.p, 0, nn * sizeof(uint32_t), s->stream));
+    PhaseClock clk(std::getenv("TPT_BUILD_TIMING") != nullptr);
 
     tpt::BuildBuffers b{};
     b.n_faces = s->n_faces;
@@ -520,9 +658,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
         HIP_OR_FAIL(hipStreamSynchronize(s->stream));
         s->any_emitter = root_emit != 0 ? 1 : 0;
     }
-    // Stack capacity: the binary DFS that pushes one sibling per level holds at
-    // most depth + 1 entries; the 4-wide ordered walk holds at most the tree's
-    // stack need (wide_bvh.cpp), 3 * ceil(depth / 2) for the LBVH's even-depth view.
+    clk.mark("lbvh");
     const uint32_t td = b.out_max_depth;
     uint32_t wide_need = 3 * ((td + 1) / 2) + 1;
     s->wide_tree = 0;
@@ -541,6 +677,7 @@ tpt_status tpt_scene_build(tpt_scene* s) {
                                    s->stream));
         HIP_OR_FAIL(hipMemcpyAsync(ltri.data(), s->tri.p, 12 * n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
         HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+        clk.mark("readback");
         // Culling exactness (trace.hip "Culling"): sliver triangles -- sin of the
         // angle at v0 between the edges rayHitTriangle uses below 1e-3 -- give
         // an arbitrary t, so they are listed (in up to 4 groups with union
@@ -629,74 +766,42 @@ tpt_status tpt_scene_build(tpt_scene* s) {
             }
             HIP_OR_FAIL(s->sliver_groups.upload(gb.data(), gb.size(), s->stream));
             HIP_OR_FAIL(s->sliver_list.upload(lst.data(), lst.size(), s->stream));
+            HIP_OR_FAIL(hipStreamSynchronize(s->stream));   // (gb and lst are freed below)
             s->n_sliver_groups = (int32_t)grp.size();
         }
-        tpt::WideParams prm;
-        prm.threads = s->build_threads;
+        clk.mark("slivers");
+        auto j = std::make_unique<HostTrees>();
+        j->n = n;
+        j->lbox = std::move(lbox);
+        j->lemit = std::move(lemit);
+        j->prm.threads = s->build_threads;
 #ifdef TPT_WIDE_SWEEP
-        prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
+        j->prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
 #endif
-        const int leaf_base = (int)n - 1;
-#ifdef TPT_WIDE_TREE_LBVH
-        const bool sah = false;   // A/B builds: keep the LBVH's even-depth view
-#else
-        const bool sah = true;
-#endif
-        if (sah) {
-            // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
-            std::vector<int> all(n);
-            for (size_t p = 0; p < n; ++p) all[p] = (int)p;
-            std::vector<float> w4;
-            int need = 0;
-            int n4 = -1;
+        j->lbvh_n4 = s->n4;
+        j->timing = clk.on;
+        if (async) {
+            s->pending_need = wide_need;
+            HostTrees* jp = j.get();
             try {
-                n4 = tpt::build_wide_sah(all, lbox.data(), lemit.data(), leaf_base, 0, w4, &need, prm);
-            } catch (const std::bad_alloc&) {
-                return fail(TPT_ERR_OOM, "traversal tree build: host allocation failed");
-            } catch (const std::exception& ex) {
-                return fail(TPT_ERR_HIP, std::string("traversal tree build: ") + ex.what());
-            }
-            if (n4 > 0 && (size_t)n4 <= n - 1 && need <= 150) {
-                HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p, w4.data(), w4.size() * sizeof(float),
-                                           hipMemcpyHostToDevice, s->stream));
-                s->n4 = n4;
-                wide_need = (uint32_t)need;
-                s->wide_tree = 1;
+                j->th = std::thread([jp] { build_host_trees(*jp); });
+                s->pending = std::move(j);
+                s->built = true;   // (finish_pending completes it)
+                return TPT_OK;
+            } catch (const std::system_error&) {   // no thread: build it here
             }
         }
-        // The direct probe's first pass (closest emissive hit, trace.hip
-        // TM_EMIT) walks a tree over the emissive triangles alone, appended
-        // after the main tree's nodes: same exact leaf boxes and positions, so
-        // the same hit as the emitter-filtered walk of the whole tree.
-        std::vector<int> em;
-        for (size_t p = 0; p < n; ++p)
-            if (lemit[p]) em.push_back((int)p);
-        if (!em.empty()) {
-            std::vector<float> e4;
-            int eneed = 0;
-            int ne4 = -1;
-            try {
-                ne4 = tpt::build_wide_sah(em, lbox.data(), lemit.data(), leaf_base, s->n4, e4, &eneed, prm);
-            } catch (const std::bad_alloc&) {
-                return fail(TPT_ERR_OOM, "emitter tree build: host allocation failed");
-            } catch (const std::exception& ex) {
-                return fail(TPT_ERR_HIP, std::string("emitter tree build: ") + ex.what());
-            }
-            if (ne4 > 0 && (size_t)(s->n4 + ne4) <= n - 1 && eneed <= 150) {
-                HIP_OR_FAIL(hipMemcpyAsync(s->inner4.p + 8 * (size_t)s->n4, e4.data(), e4.size() * sizeof(float),
-                                           hipMemcpyHostToDevice, s->stream));
-                s->emit_root = s->n4;
-                s->emit_inline = ne4 == 1 ? 1 : 0;
-                wide_need = std::max(wide_need, (uint32_t)eneed);
-            }
-        }
-        HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+        build_host_trees(*j);
+        const tpt_status st = upload_host_trees(s, *j, &wide_need);
+        if (st != TPT_OK) return st;
+        clk.mark("upload");
     }
-    s->stack_depth = (int32_t)std::max<uint32_t>(std::max<uint32_t>(td + 2, wide_need), 2);
-    if (s->stack_depth > 160) return fail(TPT_ERR_INVALID_ARG, "BVH deeper than the LDS stack supports");
-    s->built = true;
-    return TPT_OK;
+    return finish_stack(s, wide_need);
 }
+
+tpt_status tpt_scene_build(tpt_scene* s) { return scene_build(s, false); }
+
+tpt_status tpt_scene_build_async(tpt_scene* s) { return scene_build(s, true); }
 
 void tpt_scene_destroy(tpt_scene* s) { delete s; }
 
@@ -880,6 +985,12 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
             HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, fseeds[f], W, band_rows, band_count, p->band_index, bh, H,
                                              s->rng.p + f * 6 * npix, st));
     HIP_OR_FAIL(hipEventRecord(s->ev[1], st));
+    // an asynchronous scene build's host half ran while the above was enqueued
+    double tree_wait_ms = 0.0;
+    {
+        const tpt_status bs = finish_pending(s, &tree_wait_ms);
+        if (bs != TPT_OK) return bs;
+    }
     const uint64_t total_spp = (resume ? s->acc_spp : 0) + (uint64_t)p->spp;
     if (total_spp > (uint64_t)INT32_MAX) return fail(TPT_ERR_INVALID_ARG, "accumulated spp overflow");
 
@@ -1187,6 +1298,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         stats->rng_init_ms = ms;
         stats->trace_ms = trace_ms;
         stats->trace_kernel_ms = kernel_ms;
+        stats->tree_wait_ms = tree_wait_ms;
         (void)hipEventElapsedTime(&ms, s->ev[2], s->ev[3]);
         stats->resolve_ms = ms;
         stats->trace_launches = launches;
@@ -1244,6 +1356,10 @@ tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const 
                                 int32_t mode, int32_t* hit, float* t, float* uv) {
     if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
     if (mode < 0 || mode > 3) return fail(TPT_ERR_INVALID_ARG, "unknown trace mode");
+    {
+        const tpt_status bs = finish_pending(s);
+        if (bs != TPT_OK) return bs;
+    }
     if (n && (!o || !d || !hit || !t || !uv)) return fail(TPT_ERR_INVALID_ARG, "null argument");
     DeviceGuard g(s->device);
     DevBuf<float> dorg, ddir, dt, duv;

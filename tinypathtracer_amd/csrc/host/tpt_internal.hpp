@@ -3,8 +3,10 @@
 
 #include <array>
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "tpt.h"
@@ -48,13 +50,35 @@ void load_image(const std::string& path, std::vector<uint8_t>& rgba, int& w, int
 
 // SAH 4-wide traversal tree over (a subset of) the LBVH's exact leaf boxes
 // (wide_bvh.cpp): 32 floats per node in the inner4 layout; returns the node count.
+// A host vector whose resize leaves new elements uninitialised (the writer
+// fills every one), so a 6-MB tree buffer is not zero-filled first.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() noexcept = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new ((void*)p) U;
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+};
+using HostFloats = std::vector<float, NoInitAlloc<float>>;
+
 struct WideParams {
     int sweep_max = 32;    // SAH ranges up to this size use an exact sweep, larger ones 32 bins
     int threads = -1;      // build threads: < 0 the usable cores (affinity, cgroup quota); 0, 1 serial
 };
 int usable_cores();
 int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,
-                   int id_base, std::vector<float>& out, int* stack_need, const WideParams& prm);
+                   int id_base, HostFloats& out, int* stack_need, const WideParams& prm);
 
 }  // namespace tpt
 
