@@ -300,9 +300,12 @@ def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_lau
         if c.get("SQ_INSTS_VALU") and clk:
             inst = c["SQ_INSTS_VALU"] * lps / step_s / 1e9
             peak = VALU_INST_PER_CU_CYCLE * N_CU * clk
+            lu = pm.get("valu_lane_utilization")
             limits["valu_issue"] = {"achieved": round(inst, 1), "peak": round(peak, 1), "unit": "G wave-inst/s",
                                     "frac": round(inst / peak, 4), "clock_ghz": clk,
-                                    "lane_utilization": pm.get("valu_lane_utilization")}
+                                    "lane_utilization": lu,
+                                    # active-lane throughput against every lane of every SIMD issuing
+                                    "useful_lane_frac": round(inst / peak * lu, 4) if lu is not None else None}
         for k in ("sq_wait_any_frac", "sq_active_inst_any_frac", "l2_hit_rate", "l1_miss_to_l2_frac",
                   "lds_bank_conflict_cycles_per_lds_inst", "ta_accesses_per_cu_cycle"):
             if pm.get(k) is not None:
