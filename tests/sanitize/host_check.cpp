@@ -21,7 +21,7 @@
 
 #include "tpt_internal.hpp"
 
-static int check_wide(int n, unsigned seed) {
+static int check_wide(int n, unsigned seed, int threads) {
     std::mt19937 rng(seed);
     std::uniform_real_distribution<float> u(-10.0f, 10.0f), e(0.0f, 2.0f);
     std::vector<float> box(6 * (size_t)n);
@@ -41,10 +41,22 @@ static int check_wide(int n, unsigned seed) {
     tpt::HostFloats out;
     int need = 0;
     tpt::WideParams prm;
+    prm.threads = threads;
     const int nodes = tpt::build_wide_sah(pos, box.data(), emit.data(), n - 1, 0, out, &need, prm);
     if (nodes <= 0 || out.size() < 32 * (size_t)nodes || need <= 0) {
         std::printf("error: wide tree n=%d nodes=%d need=%d\n", n, nodes, need);
         return 1;
+    }
+    if (threads != 1) {   // the threaded build must equal the serial one byte for byte
+        tpt::HostFloats ser;
+        int sneed = 0;
+        prm.threads = 1;
+        const int snodes = tpt::build_wide_sah(pos, box.data(), emit.data(), n - 1, 0, ser, &sneed, prm);
+        if (snodes != nodes || sneed != need || ser.size() != out.size() ||
+            std::memcmp(ser.data(), out.data(), out.size() * sizeof(float)) != 0) {
+            std::printf("error: wide tree n=%d threads=%d differs from the serial build\n", n, threads);
+            return 1;
+        }
     }
     std::printf("ok wide n=%d nodes=%d stack=%d\n", n, nodes, need);
     return 0;
@@ -52,11 +64,12 @@ static int check_wide(int n, unsigned seed) {
 
 int main(int argc, char** argv) {
     if (argc < 3) {
-        std::fprintf(stderr, "usage: host_check gltf|image FILE... | wide N SEED\n");
+        std::fprintf(stderr, "usage: host_check gltf|image FILE... | wide N SEED [THREADS]\n");
         return 2;
     }
     const std::string mode = argv[1];
-    if (mode == "wide") return check_wide(std::atoi(argv[2]), argc > 3 ? (unsigned)std::atoi(argv[3]) : 1u);
+    if (mode == "wide")
+        return check_wide(std::atoi(argv[2]), argc > 3 ? (unsigned)std::atoi(argv[3]) : 1u, argc > 4 ? std::atoi(argv[4]) : -1);
     for (int i = 2; i < argc; ++i) {
         try {
             if (mode == "gltf") {

@@ -179,7 +179,27 @@ def test_corrupted_images(host_check, tmp_path):
     assert sum(x.startswith("error") for x in out) > len(files) // 3
 
 
-@pytest.mark.parametrize("n,seed", [(2, 1), (3, 2), (33, 3), (1000, 4), (20000, 5)])
-def test_wide_tree_builder(host_check, n, seed):
-    r = subprocess.run([host_check, "wide", str(n), str(seed)], capture_output=True, text=True, timeout=600)
+@pytest.mark.parametrize("n,seed,threads", [(2, 1, -1), (3, 2, -1), (33, 3, -1), (1000, 4, -1), (20000, 5, -1),
+                                            (20000, 6, 4)])
+def test_wide_tree_builder(host_check, n, seed, threads):
+    r = subprocess.run([host_check, "wide", str(n), str(seed), str(threads)], capture_output=True, text=True,
+                       timeout=600)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr[-3000:]
+
+
+def test_wide_tree_pool_under_tsan():
+    """The builder's task pool (chunked binning and scatter, subtree tasks,
+    the parallel breadth-first collapse) under ThreadSanitizer, 4 and 8
+    threads, each compared byte for byte with the serial build."""
+    if not os.path.isdir(SAN) or shutil.which("g++") is None:
+        pytest.skip("sanitizer harness not present (GPU box) or no g++")
+    r = subprocess.run(["make", "-C", SAN, "host_check_tsan"], capture_output=True, text=True)
+    if r.returncode != 0:
+        if "tsan" in r.stderr.lower() or "sanitize" in r.stderr.lower():
+            pytest.skip("toolchain without the TSan runtime")
+        raise AssertionError(r.stderr)
+    exe = os.path.join(SAN, "host_check_tsan")
+    for threads in (4, 8):
+        r = subprocess.run([exe, "wide", "40000", "7", str(threads)], capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+        assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr[-4000:]
