@@ -178,6 +178,12 @@ struct BuildBuffers {
 };
 hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes);
 hipError_t launch_build(BuildBuffers& b, hipStream_t s);
+// Culling exactness inputs (trace.hip "Culling"), per leaf position of the packed
+// triangles: sliver[p] = 1 when sin of the angle at v0 between e1 and e2 is below
+// 1e-3, and *coord_max (zeroed by the caller) = the bits of the largest
+// |coordinate| of any vertex as a double (positive doubles order as integers).
+hipError_t launch_sliver_scan(const float4* tri, int32_t n, uint8_t* sliver, unsigned long long* coord_max,
+                              hipStream_t s);
 
 // trace.hip
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s);

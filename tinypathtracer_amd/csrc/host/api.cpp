@@ -72,6 +72,30 @@ struct DevBuf {
     }
 };
 
+// Page-locked host memory (hipHostMalloc), grown on demand: the per-frame
+// read-back of the leaf boxes runs at copy-engine speed instead of through a
+// pageable bounce buffer.
+template <class T>
+struct HostPinned {
+    T* p = nullptr;
+    size_t n = 0;
+    HostPinned() = default;
+    HostPinned(const HostPinned&) = delete;
+    HostPinned& operator=(const HostPinned&) = delete;
+    ~HostPinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t alloc(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+};
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {
@@ -222,8 +246,8 @@ struct PhaseClock {
 // then waits for it: finish_pending).
 struct HostTrees {
     size_t n = 0;
-    std::vector<float> lbox;
-    std::vector<uint32_t> lemit;
+    const float* lbox = nullptr;      // 6 per leaf position (not owned: the scene's staging)
+    const uint32_t* lemit = nullptr;  // per leaf position
     tpt::WideParams prm;
     int32_t lbvh_n4 = 0;      // the LBVH even-depth view's node count (inner4 when no SAH tree)
     bool timing = false;
@@ -255,7 +279,7 @@ void build_host_trees(HostTrees& j) {
             // SAH 4-wide traversal tree over the LBVH's exact leaf boxes (wide_bvh.cpp)
             std::vector<int> all(n);
             for (size_t p = 0; p < n; ++p) all[p] = (int)p;
-            j.n4 = tpt::build_wide_sah(all, j.lbox.data(), j.lemit.data(), leaf_base, 0, j.w4, &j.need, j.prm);
+            j.n4 = tpt::build_wide_sah(all, j.lbox, j.lemit, leaf_base, 0, j.w4, &j.need, j.prm);
         }
         clk.mark("sah");
         // The direct probe's first pass (closest emissive hit, trace.hip
@@ -266,7 +290,7 @@ void build_host_trees(HostTrees& j) {
         for (size_t p = 0; p < n; ++p)
             if (j.lemit[p]) em.push_back((int)p);
         if (!em.empty())
-            j.ne4 = tpt::build_wide_sah(em, j.lbox.data(), j.lemit.data(), leaf_base, j.base(), j.e4, &j.eneed, j.prm);
+            j.ne4 = tpt::build_wide_sah(em, j.lbox, j.lemit, leaf_base, j.base(), j.e4, &j.eneed, j.prm);
         clk.mark("emit_tree");
     } catch (const std::bad_alloc&) {
         j.st = TPT_ERR_OOM;
@@ -298,6 +322,11 @@ struct tpt_scene {
     float cull_eps = 0.0f;                  // absolute position slack of the t-culls
     uint32_t tree_depth = 0;
     int32_t build_threads = -1;             // SAH tree build threads (tpt_scene_set_build_threads)
+    DevBuf<uint8_t> sliver_flags;           // k_sliver_scan outputs
+    DevBuf<unsigned long long> coord_max;
+    HostPinned<float> h_lbox;               // read-back staging of a build (leaf boxes, emitter flags,
+    HostPinned<uint32_t> h_lemit;           // sliver flags + coord_max); declared before `pending`, which
+    HostPinned<uint8_t> h_sliver;           // reads them and is destroyed (joined) first
     std::unique_ptr<HostTrees> pending;     // tpt_scene_build_async's host half, until finish_pending
     uint32_t pending_need = 0;              // its stack bound before the trees
     // inputs
@@ -668,16 +697,6 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
     s->n_sliver_groups = 0;
     s->cull_eps = 0.0f;
     if (n > 1 && s->boxes_finite) {
-        std::vector<float> lbox(6 * n);
-        std::vector<uint32_t> lemit(n);
-        std::vector<float> ltri(12 * n);   // packed leaf triangles (v0, fid), e1, e2 by sorted position
-        HIP_OR_FAIL(hipMemcpyAsync(lbox.data(), s->node_box.p + 6 * (n - 1), 6 * n * sizeof(float),
-                                   hipMemcpyDeviceToHost, s->stream));
-        HIP_OR_FAIL(hipMemcpyAsync(lemit.data(), s->emit.p + (n - 1), n * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                   s->stream));
-        HIP_OR_FAIL(hipMemcpyAsync(ltri.data(), s->tri.p, 12 * n * sizeof(float), hipMemcpyDeviceToHost, s->stream));
-        HIP_OR_FAIL(hipStreamSynchronize(s->stream));
-        clk.mark("readback");
         // Culling exactness (trace.hip "Culling"): sliver triangles -- sin of the
         // angle at v0 between the edges rayHitTriangle uses below 1e-3 -- give
         // an arbitrary t, so they are listed (in up to 4 groups with union
@@ -685,23 +704,33 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
         // absolute position slack is 4 ulps of the largest world coordinate (a
         // hit point, the next ray's origin, is rounded to its ulp; an edge hit
         // accepted by barycentric rounding lies a few ulps outside its triangle).
+        // Both come from k_sliver_scan; the leaf boxes and emitter flags (for
+        // the host trees) come back with them into pinned staging.
+        HIP_OR_FAIL(s->sliver_flags.alloc(n));
+        HIP_OR_FAIL(s->coord_max.alloc(1));
+        HIP_OR_FAIL(hipMemsetAsync(s->coord_max.p, 0, sizeof(unsigned long long), s->stream));
+        HIP_OR_FAIL(tpt::launch_sliver_scan(s->tri.p, (int32_t)n, s->sliver_flags.p, s->coord_max.p, s->stream));
+        HIP_OR_FAIL(s->h_lbox.alloc(6 * n));
+        HIP_OR_FAIL(s->h_lemit.alloc(n));
+        HIP_OR_FAIL(s->h_sliver.alloc(n + 8));
+        float* const lbox = s->h_lbox.p;
+        uint32_t* const lemit = s->h_lemit.p;
+        uint8_t* const lsliver = s->h_sliver.p;
+        HIP_OR_FAIL(hipMemcpyAsync(lbox, s->node_box.p + 6 * (n - 1), 6 * n * sizeof(float), hipMemcpyDeviceToHost,
+                                   s->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(lemit, s->emit.p + (n - 1), n * sizeof(uint32_t), hipMemcpyDeviceToHost, s->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(lsliver, s->sliver_flags.p, n, hipMemcpyDeviceToHost, s->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(lsliver + n, s->coord_max.p, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   s->stream));
+        HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+        clk.mark("readback");
         std::vector<int> sl;
+        for (size_t p = 0; p < n; ++p)
+            if (lsliver[p]) sl.push_back((int)p);
+        unsigned long long mbits = 0;
+        std::memcpy(&mbits, lsliver + n, sizeof mbits);
         double max_coord = 0.0;
-        for (size_t p = 0; p < n; ++p) {
-            const float* q = &ltri[12 * p];
-            const double a[3] = {q[4], q[5], q[6]}, b[3] = {q[8], q[9], q[10]};
-            const double c[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
-            const double la = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
-            const double lb = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
-            const double lc = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
-            for (int k = 0; k < 3; ++k)
-                max_coord = std::max(max_coord, std::max(std::fabs((double)q[k]),
-                                                          std::max(std::fabs((double)q[k] + a[k]),
-                                                                   std::fabs((double)q[k] + b[k]))));
-            // (an edge of exactly zero length makes rayHitTriangle's determinant
-            // exactly 0, or NaN with t NaN: never accepted, so not a sliver here)
-            if (la > 0.0 && lb > 0.0 && !(lc >= 1e-3 * la * lb)) sl.push_back((int)p);   // NaN-safe
-        }
+        std::memcpy(&max_coord, &mbits, sizeof max_coord);
         s->slivers = (int32_t)sl.size();
         s->cull_eps = 0.0f;
         if (std::isfinite(max_coord) && max_coord > 0.0) {
@@ -772,8 +801,8 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
         clk.mark("slivers");
         auto j = std::make_unique<HostTrees>();
         j->n = n;
-        j->lbox = std::move(lbox);
-        j->lemit = std::move(lemit);
+        j->lbox = lbox;     // the scene's pinned staging: the next build joins this job first
+        j->lemit = lemit;
         j->prm.threads = s->build_threads;
 #ifdef TPT_WIDE_SWEEP
         j->prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold

@@ -138,8 +138,8 @@ struct Uninit {
 };
 
 // The build's worker threads: a FIFO of tasks run by threads - 1 workers and
-// by whichever thread waits on a task group (it runs queued tasks instead of
-// sleeping, so nested waits cannot deadlock).  Threads are started once per
+// by whichever thread waits on a task group (it runs queued tasks while there
+// are any, so nested waits cannot deadlock, and sleeps otherwise).  Threads are started once per
 // build: on the GPU box starting one costs ≈ 35 µs, 15 at once ≈ 0.6 ms.  A
 // thread that cannot be started (std::system_error under a pid or ulimit cap)
 // just leaves its share to the others; tasks must not throw.
@@ -170,13 +170,17 @@ public:
             q_.push_back(std::move(f));
         }
         cv_.notify_one();
+        done_cv_.notify_all();   // a waiter may run it
     }
     // Runs queued tasks until every submitted task (and what they submit) is done.
     void wait_all() { help_until(pending_); }
     // Runs queued tasks until `left` reaches 0.
     void help_until(const std::atomic<int>& left) {
-        while (left.load(std::memory_order_acquire) > 0)
-            if (!run_one()) std::this_thread::yield();
+        while (left.load(std::memory_order_acquire) > 0) {
+            if (run_one()) continue;
+            std::unique_lock<std::mutex> g(mu_);
+            done_cv_.wait(g, [&] { return left.load(std::memory_order_acquire) == 0 || !q_.empty(); });
+        }
     }
     // f(c) for c in [0, nc), chunk 0 on this thread; returns when all are done.
     template <class F>
@@ -201,8 +205,15 @@ private:
             q_.pop_front();
         }
         f();
-        pending_.fetch_sub(1, std::memory_order_acq_rel);
+        finished();
         return true;
+    }
+    // After a task: its counters have moved; wake the waiters (the empty
+    // critical section orders this against a waiter's predicate check).
+    void finished() {
+        pending_.fetch_sub(1, std::memory_order_acq_rel);
+        { std::lock_guard<std::mutex> g(mu_); }
+        done_cv_.notify_all();
     }
     void work() {
         for (;;) {
@@ -215,12 +226,13 @@ private:
                 q_.pop_front();
             }
             f();
-            pending_.fetch_sub(1, std::memory_order_acq_rel);
+            finished();
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
-    std::condition_variable cv_;
+    std::condition_variable cv_;        // workers: a task is queued (or stop)
+    std::condition_variable done_cv_;   // waiters: a task finished or was queued
     std::deque<std::function<void()>> q_;
     std::atomic<int> pending_{0};
     bool stop_ = false;
@@ -636,31 +648,39 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
                      std::chrono::duration<double, std::milli>(t - t_last).count());
         t_last = t;
     };
-    Builder B;
-    B.sweep_max = prm.sweep_max;
-    B.buf[0].reset(n);
-    B.buf[1].reset(n);
-    for (int i = 0; i < n; ++i) {
-        const int p = pos[i];
-        Rec& q = B.buf[0][i];
-        for (int k = 0; k < 3; ++k) {
-            q.lo[k] = leaf_box[6 * p + k];
-            q.hi[k] = leaf_box[6 * p + 3 + k];
-        }
-        q.pos = p;
-        q.pad = 0.0f;
-    }
-    VBox cb;
-    cb.empty();
-    Builder::cen_bounds(&B.buf[0][0], n, cb);
-    B.nodes.reset(2 * (size_t)n - 1);
-    B.D.reset(B.nodes.size());
-    B.pick.reset(B.nodes.size());
     // threads: at most prm.threads (< 0: the cores this process may use; 0 or
     // 1: a serial build -- the same tree), and about one per 4 K leaves
     const int hw = std::max(1, std::min(prm.threads < 0 ? usable_cores() : prm.threads, 64));
     Pool pool(std::min(hw, n / 4096 + 1));
+    Builder B;
     B.pool = &pool;
+    B.sweep_max = prm.sweep_max;
+    B.buf[0].reset(n);
+    B.buf[1].reset(n);
+    // the leaf records and the root's centroid bounds, in chunks (merged exactly)
+    const int nc = std::max(1, std::min(pool.threads(), n / Builder::kParChunk));
+    std::vector<VBox> cbs(nc);
+    pool.chunks(nc, [&](int c) {
+        const int i0 = (int)((int64_t)n * c / nc), i1 = (int)((int64_t)n * (c + 1) / nc);
+        for (int i = i0; i < i1; ++i) {
+            const int p = pos[i];
+            Rec& q = B.buf[0][i];
+            for (int k = 0; k < 3; ++k) {
+                q.lo[k] = leaf_box[6 * p + k];
+                q.hi[k] = leaf_box[6 * p + 3 + k];
+            }
+            q.pos = p;
+            q.pad = 0.0f;
+        }
+        cbs[c].empty();
+        Builder::cen_bounds(&B.buf[0][i0], i1 - i0, cbs[c]);
+    });
+    VBox cb;
+    cb.empty();
+    for (const VBox& x : cbs) cb.grow(x);
+    B.nodes.reset(2 * (size_t)n - 1);
+    B.D.reset(B.nodes.size());
+    B.pick.reset(B.nodes.size());
     const int root = 0;
     mark("setup");
     if (n >= Builder::kTask) {

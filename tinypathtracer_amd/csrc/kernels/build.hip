@@ -332,6 +332,44 @@ __global__ void k_pack_nodes36(BuildBuffers b) {
     for (int k = 0; k < 6; ++k) o[3 + k] = __float_as_uint(bx[k]);
 }
 
+// The host's sliver criterion and cull-slack scale, in double as it computed
+// them: a sliver's |e1 x e2| < 1e-3 |e1| |e2| (a zero-length edge makes the
+// determinant exactly 0 or NaN: never accepted, so not a sliver); the largest
+// |v0|, |v0 + e1|, |v0 + e2| coordinate, reduced per block, then one 64-bit
+// atomic max per block.
+__global__ __launch_bounds__(256) void k_sliver_scan(const float4* __restrict__ tri, int n, uint8_t* __restrict__ sliver,
+                                                     unsigned long long* coord_max) {
+    __shared__ double smax[256];
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    double m = 0.0;
+    if (p < n) {
+        const float4 q0 = tri[3 * p], q1 = tri[3 * p + 1], q2 = tri[3 * p + 2];
+        const double a0 = q1.x, a1 = q1.y, a2 = q1.z, b0 = q2.x, b1 = q2.y, b2 = q2.z;
+        const double c0 = a1 * b2 - a2 * b1, c1 = a2 * b0 - a0 * b2, c2 = a0 * b1 - a1 * b0;
+        const double la = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
+        const double lb = sqrt(b0 * b0 + b1 * b1 + b2 * b2);
+        const double lc = sqrt(c0 * c0 + c1 * c1 + c2 * c2);
+        sliver[p] = (la > 0.0 && lb > 0.0 && !(lc >= 1e-3 * la * lb)) ? 1 : 0;   // NaN-safe
+        const double v[3] = {q0.x, q0.y, q0.z}, a[3] = {a0, a1, a2}, b[3] = {b0, b1, b2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) m = fmax(m, fmax(fabs(v[k]), fmax(fabs(v[k] + a[k]), fabs(v[k] + b[k]))));
+    }
+    smax[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) smax[threadIdx.x] = fmax(smax[threadIdx.x], smax[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(coord_max, (unsigned long long)__double_as_longlong(smax[0]));
+}
+
+hipError_t launch_sliver_scan(const float4* tri, int32_t n, uint8_t* sliver, unsigned long long* coord_max,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sliver_scan, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tri, n, sliver, coord_max);
+    return hipGetLastError();
+}
+
 hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes) {
     // the Morton sort (63 bits) and the breadth-first numbering sort (64 bits) share the buffer
     size_t a = 0, b = 0;
