@@ -58,6 +58,25 @@ static int check_wide(int n, unsigned seed, int threads) {
             return 1;
         }
     }
+    {   // a reused workspace (the scene's, frame after frame) builds the same tree,
+        // also after a build of another size in it
+        tpt::WideWorkspace ws;
+        tpt::WideParams wp;
+        wp.threads = threads;
+        wp.ws = &ws;
+        std::vector<int> half(pos.begin(), pos.begin() + (n + 1) / 2);
+        for (int rep = 0; rep < 3; ++rep) {
+            tpt::HostFloats o2;
+            int n2 = 0;
+            const std::vector<int>& pp = rep == 1 ? half : pos;
+            const int k = tpt::build_wide_sah(pp, box.data(), emit.data(), n - 1, 0, o2, &n2, wp);
+            if (rep != 1 && (k != nodes || n2 != need || o2.size() != out.size() ||
+                             std::memcmp(o2.data(), out.data(), out.size() * sizeof(float)) != 0)) {
+                std::printf("error: wide tree n=%d: a reused workspace builds another tree\n", n);
+                return 1;
+            }
+        }
+    }
     std::printf("ok wide n=%d nodes=%d stack=%d\n", n, nodes, need);
     return 0;
 }

@@ -240,10 +240,12 @@ struct PhaseClock {
 };
 
 // The host half of a scene build: the SAH traversal trees over the LBVH's leaf
-// boxes (wide_bvh.cpp).  Pure host work on its own copies -- no HIP call, no
-// access to the scene -- so tpt_scene_build_async runs it on a thread of its
-// own while the caller goes on (tpt_render enqueues the RNG initialisation,
-// then waits for it: finish_pending).
+// boxes (wide_bvh.cpp).  Pure host work -- no HIP call, no access to the scene
+// but its read-back staging -- so tpt_scene_build_async runs it on a thread of
+// its own while the caller goes on (tpt_render enqueues the RNG
+// initialisation, then waits for it: finish_pending).  One per scene, kept
+// between builds with its work arrays and output buffers (no per-frame
+// allocation to fault in).
 struct HostTrees {
     size_t n = 0;
     const float* lbox = nullptr;      // 6 per leaf position (not owned: the scene's staging)
@@ -256,9 +258,20 @@ struct HostTrees {
     int n4 = -1, need = 0, ne4 = -1, eneed = 0;
     tpt_status st = TPT_OK;
     std::string msg;
+    tpt::WideWorkspace ws;
     std::thread th;
-    ~HostTrees() {
+    ~HostTrees() { join(); }
+    void join() {
         if (th.joinable()) th.join();
+    }
+    void reset_results() {
+        n4 = -1;
+        need = 0;
+        ne4 = -1;
+        eneed = 0;
+        st = TPT_OK;
+        msg.clear();
+        prm.ws = &ws;
     }
     bool main_ok() const { return n4 > 0 && (size_t)n4 <= n - 1 && need <= 150; }
     int32_t base() const { return main_ok() ? n4 : lbvh_n4; }   // the emitter tree's first id
@@ -325,9 +338,10 @@ struct tpt_scene {
     DevBuf<uint8_t> sliver_flags;           // k_sliver_scan outputs
     DevBuf<unsigned long long> coord_max;
     HostPinned<float> h_lbox;               // read-back staging of a build (leaf boxes, emitter flags,
-    HostPinned<uint32_t> h_lemit;           // sliver flags + coord_max); declared before `pending`, which
+    HostPinned<uint32_t> h_lemit;           // sliver flags + coord_max); declared before `trees`, which
     HostPinned<uint8_t> h_sliver;           // reads them and is destroyed (joined) first
-    std::unique_ptr<HostTrees> pending;     // tpt_scene_build_async's host half, until finish_pending
+    std::unique_ptr<HostTrees> trees;       // the host half of the builds
+    bool pending = false;                   // tpt_scene_build_async's host half runs / is not uploaded yet
     uint32_t pending_need = 0;              // its stack bound before the trees
     // inputs
     DevBuf<uint32_t> indices;
@@ -592,12 +606,13 @@ tpt_status finish_stack(tpt_scene* s, uint32_t wide_need) {
 static tpt_status finish_pending(tpt_scene* s, double* wait_ms = nullptr) {
     if (!s->pending) return TPT_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    std::unique_ptr<HostTrees> j = std::move(s->pending);
-    if (j->th.joinable()) j->th.join();
+    HostTrees& j = *s->trees;
+    j.join();
+    s->pending = false;
     if (wait_ms) *wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     DeviceGuard g(s->device);
     uint32_t wide_need = s->pending_need;
-    tpt_status st = upload_host_trees(s, *j, &wide_need);
+    tpt_status st = upload_host_trees(s, j, &wide_need);
     if (st == TPT_OK) st = finish_stack(s, wide_need);
     if (st != TPT_OK) s->built = false;
     return st;
@@ -605,7 +620,8 @@ static tpt_status finish_pending(tpt_scene* s, double* wait_ms = nullptr) {
 
 static tpt_status scene_build(tpt_scene* s, bool async) {
     if (!s) return fail(TPT_ERR_INVALID_ARG, "null scene");
-    s->pending.reset();   // a previous asynchronous build still running: its trees are superseded
+    if (s->trees) s->trees->join();   // a previous asynchronous build still running: its trees are superseded
+    s->pending = false;
     s->built = false;
     DeviceGuard g(s->device);
     const size_t n = (size_t)s->n_faces, nn = 2 * n - 1, nv = (size_t)s->n_vertices;
@@ -799,29 +815,37 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
             s->n_sliver_groups = (int32_t)grp.size();
         }
         clk.mark("slivers");
-        auto j = std::make_unique<HostTrees>();
-        j->n = n;
-        j->lbox = lbox;     // the scene's pinned staging: the next build joins this job first
-        j->lemit = lemit;
-        j->prm.threads = s->build_threads;
+        if (!s->trees) {
+            try {
+                s->trees = std::make_unique<HostTrees>();
+            } catch (const std::bad_alloc&) {
+                return fail(TPT_ERR_OOM, "traversal tree build: host allocation failed");
+            }
+        }
+        HostTrees& j = *s->trees;
+        j.reset_results();
+        j.n = n;
+        j.lbox = lbox;     // the scene's pinned staging: the next build joins this job first
+        j.lemit = lemit;
+        j.prm.threads = s->build_threads;
 #ifdef TPT_WIDE_SWEEP
-        j->prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
+        j.prm.sweep_max = TPT_WIDE_SWEEP;   // A/B builds: exact-sweep threshold
 #endif
-        j->lbvh_n4 = s->n4;
-        j->timing = clk.on;
+        j.lbvh_n4 = s->n4;
+        j.timing = clk.on;
         if (async) {
             s->pending_need = wide_need;
-            HostTrees* jp = j.get();
+            HostTrees* jp = &j;
             try {
-                j->th = std::thread([jp] { build_host_trees(*jp); });
-                s->pending = std::move(j);
+                j.th = std::thread([jp] { build_host_trees(*jp); });
+                s->pending = true;
                 s->built = true;   // (finish_pending completes it)
                 return TPT_OK;
             } catch (const std::system_error&) {   // no thread: build it here
             }
         }
-        build_host_trees(*j);
-        const tpt_status st = upload_host_trees(s, *j, &wide_need);
+        build_host_trees(j);
+        const tpt_status st = upload_host_trees(s, j, &wide_need);
         if (st != TPT_OK) return st;
         clk.mark("upload");
     }

@@ -72,9 +72,21 @@ struct NoInitAlloc : std::allocator<T> {
 };
 using HostFloats = std::vector<float, NoInitAlloc<float>>;
 
+// The build's work arrays (≈ 30 MB for 131 K leaves), kept between the builds
+// of a scene: a fresh allocation is first touched page by page every frame.
+struct WideWorkspace {
+    struct Impl;
+    std::unique_ptr<Impl> impl;
+    WideWorkspace();
+    ~WideWorkspace();
+    WideWorkspace(const WideWorkspace&) = delete;
+    WideWorkspace& operator=(const WideWorkspace&) = delete;
+};
+
 struct WideParams {
     int sweep_max = 32;    // SAH ranges up to this size use an exact sweep, larger ones 32 bins
     int threads = -1;      // build threads: < 0 the usable cores (affinity, cgroup quota); 0, 1 serial
+    WideWorkspace* ws = nullptr;   // reused work arrays (nullptr: the build's own); one build at a time
 };
 int usable_cores();
 int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uint32_t* leaf_emit, int leaf_base,

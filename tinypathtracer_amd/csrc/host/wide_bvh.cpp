@@ -118,7 +118,15 @@ struct VBox {
         }
         return b;
     }
-    double area() const { return box().area(); }
+    // Box::area on the vectors: the same double subtractions and products
+    double area() const {
+        const __m128d l01 = _mm_cvtps_pd(lo), h01 = _mm_cvtps_pd(hi);
+        const __m128d l2 = _mm_cvtps_pd(_mm_movehl_ps(lo, lo)), h2 = _mm_cvtps_pd(_mm_movehl_ps(hi, hi));
+        const __m128d d01 = _mm_sub_pd(h01, l01), d2 = _mm_sub_pd(h2, l2);
+        const double dx = _mm_cvtsd_f64(d01), dy = _mm_cvtsd_f64(_mm_unpackhi_pd(d01, d01)), dz = _mm_cvtsd_f64(d2);
+        if (!(dx >= 0.0) || !(dy >= 0.0) || !(dz >= 0.0)) return 0.0;
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
 };
 
 // A build array left uninitialised: the build writes every element it reads,
@@ -127,10 +135,20 @@ struct VBox {
 template <class T>
 struct Uninit {
     std::unique_ptr<T[]> p;
-    size_t n = 0;
-    void reset(size_t m) {
-        p.reset(new T[m]);
+    size_t n = 0, cap = 0;
+    void reset(size_t m) {   // m elements; the storage is reused when it holds them
+        if (m > cap) {
+            p.reset();
+            cap = 0;
+            p.reset(new T[m]);
+            cap = m;
+        }
         n = m;
+    }
+    void swap(Uninit& o) {
+        p.swap(o.p);
+        std::swap(n, o.n);
+        std::swap(cap, o.cap);
     }
     T& operator[](size_t i) { return p[i]; }
     const T& operator[](size_t i) const { return p[i]; }
@@ -239,6 +257,7 @@ private:
 };
 
 constexpr int kBins = 32;
+constexpr int kMaxThreads = 64;   // build threads at most (build_wide_sah)
 
 struct alignas(16) Bins {   // the binned-SAH histogram of a range, all three axes
     VBox bb[3][kBins];
@@ -394,9 +413,14 @@ struct Builder {
         }
         const __m128 clo = cb.lo, scale = _mm_load_ps(sc4);
         auto chunk_lo = [&](int c) { return b + (int)((int64_t)m * c / nc); };
-        std::vector<Bins> part(nc + 1);
+        // nc == 1 (every range below 2 chunks): one histogram on the stack, no
+        // allocation, copy or merge -- a split of 33..16 K leaves is mostly this
+        Bins one;
+        std::vector<Bins> many;   // nc > 1: [0] the merged histogram, [c + 1] chunk c's
+        if (nc > 1) many.resize(nc + 1);
+        auto hist = [&](int c) -> Bins& { return nc > 1 ? many[c + 1] : one; };
         pool->chunks(nc, [&](int c) {
-            Bins& h = part[c + 1];
+            Bins& h = hist(c);
             h.clear();
             const int i1 = chunk_lo(c + 1);
             for (int i = chunk_lo(c); i < i1; ++i) {
@@ -410,9 +434,11 @@ struct Builder {
                 }
             }
         });
-        Bins& h = part[0];
-        h = part[1];
-        for (int c = 1; c < nc; ++c) h.merge(part[c + 1]);
+        Bins& h = nc > 1 ? many[0] : one;
+        if (nc > 1) {
+            h = many[1];
+            for (int c = 1; c < nc; ++c) h.merge(many[c + 1]);
+        }
         for (int axis = 0; axis < 3; ++axis) {
             if (!live[axis]) continue;
             double ra[kBins];
@@ -450,15 +476,17 @@ struct Builder {
         }
         const int ax = best_axis;
         // each chunk's left count from its own histogram
-        std::vector<int> nl(nc + 1, 0);
+        int nl[kMaxThreads + 1];   // (nc <= the pool's threads <= kMaxThreads)
+        nl[0] = 0;
         for (int c = 0; c < nc; ++c) {
             int k = 0;
-            for (int j = 0; j < best_m; ++j) k += part[c + 1].bn[ax][j];
+            const Bins& hc = hist(c);
+            for (int j = 0; j < best_m; ++j) k += hc.bn[ax][j];
             nl[c + 1] = nl[c] + k;
         }
         const int s = b + nl[nc];
         Rec* dst = &buf[*w ^ 1][0];
-        std::vector<VBox> bl(nc), br(nc);
+        VBox bl[kMaxThreads], br[kMaxThreads];
         pool->chunks(nc, [&](int c) {
             const int i0 = chunk_lo(c), i1 = chunk_lo(c + 1);
             int ol = b + nl[c], orr = s + (i0 - b - nl[c]);
@@ -605,6 +633,39 @@ struct Builder {
 
 }  // namespace
 
+struct WideWorkspace::Impl {
+    Uninit<BNode> nodes;
+    Uninit<Rec> buf[2];
+    Uninit<std::array<double, 5>> D;
+    Uninit<std::array<int8_t, 5>> pick;
+    Uninit<int> wide_of;
+};
+WideWorkspace::WideWorkspace() : impl(new Impl) {}
+WideWorkspace::~WideWorkspace() = default;
+
+namespace {
+// Lends a workspace's arrays to a build and takes them back (also when the
+// build throws: the storage is kept for the next one).
+struct Lend {
+    WideWorkspace::Impl* w;
+    Builder& b;
+    Uninit<int>& wide_of;
+    Lend(WideWorkspace* ws, Builder& b_, Uninit<int>& wo) : w(ws ? ws->impl.get() : nullptr), b(b_), wide_of(wo) {
+        swap_all();
+    }
+    ~Lend() { swap_all(); }
+    void swap_all() {
+        if (!w) return;
+        b.nodes.swap(w->nodes);
+        b.buf[0].swap(w->buf[0]);
+        b.buf[1].swap(w->buf[1]);
+        b.D.swap(w->D);
+        b.pick.swap(w->pick);
+        wide_of.swap(w->wide_of);
+    }
+};
+}  // namespace
+
 // Host cores this process may use: its CPU affinity mask, capped by a cgroup v2
 // CPU quota (/sys/fs/cgroup/cpu.max).  std::thread::hardware_concurrency()
 // reports every CPU of the host (256 on the GPU box, whose quota is 16).
@@ -650,9 +711,11 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
     };
     // threads: at most prm.threads (< 0: the cores this process may use; 0 or
     // 1: a serial build -- the same tree), and about one per 4 K leaves
-    const int hw = std::max(1, std::min(prm.threads < 0 ? usable_cores() : prm.threads, 64));
+    const int hw = std::max(1, std::min(prm.threads < 0 ? usable_cores() : prm.threads, kMaxThreads));
     Pool pool(std::min(hw, n / 4096 + 1));
     Builder B;
+    Uninit<int> wide_of;   // binary node -> 4-wide node id (set for every node that becomes one)
+    Lend lend(prm.ws, B, wide_of);
     B.pool = &pool;
     B.sweep_max = prm.sweep_max;
     B.buf[0].reset(n);
@@ -816,7 +879,6 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
             first[t][d] = total;
             if (d < lists[t].size()) total += (int)lists[t][d].size();
         }
-    Uninit<int> wide_of;   // binary node -> 4-wide node id (set for every node that becomes one)
     wide_of.reset(N.size());
     for (size_t i = 0; i < top.size(); ++i) wide_of[top[i].b] = (int)i;
     out.resize(32 * (size_t)total);
