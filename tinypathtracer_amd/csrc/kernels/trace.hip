@@ -471,14 +471,15 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
         // (DRAIN variants) the leaves' triangles are loaded together, before any
         // test: the node's links are the same for every lane, so these are
         // uniform loads issued at once instead of one round trip per leaf
-        float k0, k1, k2, k3, e0, e1, e2, e3;
-        slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
-        slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
-        slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
-        slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
         const float hi = kRealMax, hd = 0.5f * kDelta;
         const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
                   i3 = __float_as_int(q6.w);
+        // (empty slots -- uniform -- skip their slab test; their verdict below is false)
+        float k0 = 0.0f, k1 = 0.0f, k2 = 0.0f, k3 = 0.0f, e0 = 0.0f, e1 = 0.0f, e2 = 0.0f, e3 = 0.0f;
+        if (i0 >= 0) slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
+        if (i1 >= 0) slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
+        if (i2 >= 0) slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
+        if (i3 >= 0) slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
         const int p0 = i0 >= 0 ? (i0 & kLinkMask) - nint : 0, p1 = i1 >= 0 ? (i1 & kLinkMask) - nint : 0,
                   p2 = i2 >= 0 ? (i2 & kLinkMask) - nint : 0, p3 = i3 >= 0 ? (i3 & kLinkMask) - nint : 0;
         const float4 a0 = tri[3 * p0], a1 = tri[3 * p0 + 1], a2 = tri[3 * p0 + 2];
@@ -500,19 +501,29 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
         if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test_q<true>(r, d0, d1, d2, p3, cull_eps); }
         return;
     }
-    float k0, k1, k2, k3, e0, e1, e2, e3;
-    slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
-    slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
-    slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k2, e2);
-    slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
     const float hi = kRealMax;   // nothing hit yet: r.t = FLT_MAX
     const float hd = 0.5f * kDelta;
+    // the node is the same for every lane (links uniform): a child slot that is
+    // empty (-1, fewer than 4 emitters) skips its slab test as a whole wave
     const int i0 = __float_as_int(q6.x), i1 = __float_as_int(q6.y), i2 = __float_as_int(q6.z),
               i3 = __float_as_int(q6.w);
-    if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint, cull_eps); }
-    if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint, cull_eps); }
-    if ((i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint, cull_eps); }
-    if ((i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi))) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint, cull_eps); }
+    float k, e;
+    if (i0 >= 0) {
+        slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k, e);
+        if (fmaxf(k, hd) <= fminf(e, hi)) { ++c_leaf; leaf_test<true>(r, tri, (i0 & kLinkMask) - nint, cull_eps); }
+    }
+    if (i1 >= 0) {
+        slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k, e);
+        if (fmaxf(k, hd) <= fminf(e, hi)) { ++c_leaf; leaf_test<true>(r, tri, (i1 & kLinkMask) - nint, cull_eps); }
+    }
+    if (i2 >= 0) {
+        slab_minmax(r.o, r.inv, q3.x, q3.y, q3.z, q3.w, q4.x, q4.y, k, e);
+        if (fmaxf(k, hd) <= fminf(e, hi)) { ++c_leaf; leaf_test<true>(r, tri, (i2 & kLinkMask) - nint, cull_eps); }
+    }
+    if (i3 >= 0) {
+        slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k, e);
+        if (fmaxf(k, hd) <= fminf(e, hi)) { ++c_leaf; leaf_test<true>(r, tri, (i3 & kLinkMask) - nint, cull_eps); }
+    }
 }
 
 // Slivers (Culling): the triangles the culled traversal cannot be trusted to
