@@ -256,7 +256,10 @@ private:
     bool stop_ = false;
 };
 
-constexpr int kBins = 32;
+#ifndef TPT_WIDE_BINS
+#define TPT_WIDE_BINS 32   // (A/B builds: other bin counts)
+#endif
+constexpr int kBins = TPT_WIDE_BINS;
 constexpr int kMaxThreads = 64;   // build threads at most (build_wide_sah)
 
 struct alignas(16) Bins {   // the binned-SAH histogram of a range, all three axes
