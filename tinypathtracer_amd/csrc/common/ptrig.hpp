@@ -160,4 +160,73 @@ TPT_HD void psincos2pi(float phi, float& s, float& c) {
 TPT_HD float patan2_fast(float y, float x) { return (float)datan2((double)y, (double)x); }
 TPT_HD float pacos_fast(float y) { return (float)dacos((double)y); }
 
+// ---------------------------------------------------------------------------
+// The env lookup's texel indices without the double evaluation where it cannot
+// matter.  The lookup (env_light.cuh:72-78 via Vec2UV) only keeps
+//   ix = clamp(floor(fl(u * w))), u = fl(A / fl(2 pi)) (+ 1 when < 0), A = (float)atan2_d(z, x)
+//   iy = clamp(floor(fl(v * h))), v = 1 - fl(C / pi),                  C = (float)acos_d(y)
+// and every step after A (or C) is monotonic in it (IEEE rounding is monotonic;
+// the +1 only applies on one side of 0).  An fp32 approximation a with
+// |a - A| <= kEnvTrigBound puts A in [a - bound, a + bound]; when both ends of
+// that interval give the same index (and the same side of u = 0), so does A,
+// exactly.  Otherwise (about 0.1 % of lookups: within ~1e-3 of a texel edge)
+// the caller evaluates the double path.  tests/test_cpu_math.py measures the
+// approximations' error (< 4e-7 rad) against the 4e-6 bound and checks the
+// indices against the double path on adversarial and random directions.
+constexpr float kEnvTrigBound = 4.0e-6f;
+
+// atan(t) for t in [0, 1] (Cephes atanf reduction at tan(pi/8) and minimax
+// polynomial; every step an explicit fmaf, mul or correctly rounded divide)
+TPT_HD float fatan01(float t) {
+    float off = 0.0f;
+    if (t > 0.414213562f) {
+        t = (t - 1.0f) / (t + 1.0f);
+        off = 0.785398163f;
+    }
+    const float z = t * t;
+    float p = ffma(z, 8.05374449538e-2f, -1.38776856032e-1f);
+    p = ffma(z, p, 1.99777106478e-1f);
+    p = ffma(z, p, -3.33329491539e-1f);
+    return off + ffma(p * z, t, t);
+}
+// atan2(y, x) for finite y, x with max(|x|, |y|) >= 1e-18 (else: no bound claimed)
+TPT_HD float fatan2_approx(float y, float x) {
+    const float ax = x < 0.0f ? -x : x, ay = y < 0.0f ? -y : y;
+    const float mx = ax > ay ? ax : ay, mn = ax > ay ? ay : ax;
+    float a = fatan01(mn / mx);
+    if (ay > ax) a = 1.57079633f - a;
+    if (x < 0.0f) a = 3.14159265f - a;
+    return __builtin_signbit(y) ? -a : a;   // atan2(-0, x < 0) = -pi
+}
+TPT_HD bool env_fast_ok(float v) { return v == v && v - v == 0.0f; }   // finite
+
+// The lookup's column of direction (x, z) in a w-texel row, or -1 if undecided.
+TPT_HD int env_col_fast(float z, float x, int w) {
+    const float ax = x < 0.0f ? -x : x, az = z < 0.0f ? -z : z;
+    if (!env_fast_ok(x) || !env_fast_ok(z) || !((ax > az ? ax : az) >= 1e-18f)) return -1;
+    const float a = fatan2_approx(z, x);
+    float ul = (a - kEnvTrigBound) / (2.0f * kPi), uh = (a + kEnvTrigBound) / (2.0f * kPi);
+    if ((ul < 0.0f) != (uh < 0.0f)) return -1;
+    if (ul < 0.0f) {
+        ul += 1.0f;
+        uh += 1.0f;
+    }
+    int il = (int)floorf(ul * (float)w), ih = (int)floorf(uh * (float)w);
+    il = il < 0 ? 0 : (il > w - 1 ? w - 1 : il);
+    ih = ih < 0 ? 0 : (ih > w - 1 ? w - 1 : ih);
+    return il == ih ? il : -1;
+}
+// The lookup's row of direction component y (clamped to [-1, 1]) in h rows, or -1.
+TPT_HD int env_row_fast(float y, int h) {
+    if (!env_fast_ok(y)) return -1;
+    const float c = y > 1.0f ? 1.0f : (y < -1.0f ? -1.0f : y);
+    const float s = sqrtf((1.0f - c) * (1.0f + c));
+    const float a = fatan2_approx(s, c);   // acos(c) = atan2(sqrt(1 - c^2), c), c = 0 included
+    const float vh = 1.0f - (a - kEnvTrigBound) / kPi, vl = 1.0f - (a + kEnvTrigBound) / kPi;
+    int il = (int)floorf(vl * (float)h), ih = (int)floorf(vh * (float)h);
+    il = il < 0 ? 0 : (il > h - 1 ? h - 1 : il);
+    ih = ih < 0 ? 0 : (ih > h - 1 ? h - 1 : ih);
+    return il == ih ? il : -1;
+}
+
 }  // namespace tpt

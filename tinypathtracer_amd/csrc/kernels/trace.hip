@@ -69,6 +69,9 @@
 // DRAIN variants (launches that cannot fill the chip: a few waves per SIMD anyway)
 #define TPT_TRACE_WAVES_DRAIN 4
 #endif
+#ifndef TPT_ENV_FAST
+#define TPT_ENV_FAST 1     // env texel indices from fp32 bounds, double trig only near texel edges (0: A/B builds)
+#endif
 #ifndef TPT_ENV_INLINE
 #define TPT_ENV_INLINE 0   // 1: env_lookup inlined in every variant (A/B builds)
 #endif
@@ -681,13 +684,22 @@ __device__ __forceinline__ void light_sample(const DevLight* __restrict__ Ls, in
 // sampleEnvLights (:288-294): Vec2UV (env_light.cuh:72-78) + point/clamp fetch
 // (texture.cu:156-170) of the RGBA8 equirect, row 0 = bottom.
 __device__ __forceinline__ V3 env_lookup_inl(const uint32_t* __restrict__ env, int w, int h, V3 d) {
-    float u = patan2_fast(d.z, d.x) / (2.0f * kPi);
-    if (u < 0.0f) u += 1.0f;
-    const float v = 1.0f - pacos_fast(fclamp(d.y, 1.0f, -1.0f)) / kPi;
-    int ix = (int)floorf(u * (float)w);
-    int iy = (int)floorf(v * (float)h);
-    ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
-    iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
+    // the texel indices from fp32 bounds (ptrig.hpp env_col_fast / env_row_fast:
+    // the same indices as the double evaluation wherever they decide); the
+    // double path only within ~1e-3 texel of an edge
+    int ix = TPT_ENV_FAST ? env_col_fast(d.z, d.x, w) : -1;
+    int iy = TPT_ENV_FAST ? env_row_fast(d.y, h) : -1;
+    if (ix < 0) {
+        float u = patan2_fast(d.z, d.x) / (2.0f * kPi);
+        if (u < 0.0f) u += 1.0f;
+        ix = (int)floorf(u * (float)w);
+        ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
+    }
+    if (iy < 0) {
+        const float v = 1.0f - pacos_fast(fclamp(d.y, 1.0f, -1.0f)) / kPi;
+        iy = (int)floorf(v * (float)h);
+        iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
+    }
     const uint32_t t = env[(size_t)iy * (size_t)w + (size_t)ix];
     return (1.0f / 255.0f) * v3((float)(t & 0xffu), (float)((t >> 8) & 0xffu), (float)((t >> 16) & 0xffu));
 }
