@@ -23,11 +23,20 @@ from tests.conftest import ROOT, SCENE_DIR
 SAN = os.path.join(ROOT, "tests", "sanitize")
 
 
+def _make(target):
+    """make under an exclusive lock: pytest-xdist workers each set the module's
+    fixtures up, and two concurrent links of one binary fail ("Text file busy")."""
+    import fcntl
+    with open(os.path.join(SAN, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        return subprocess.run(["make", "-C", SAN, target], capture_output=True, text=True)
+
+
 @pytest.fixture(scope="module")
 def host_check():
     if not os.path.isdir(SAN) or shutil.which("g++") is None:
         pytest.skip("sanitizer harness not present (GPU box) or no g++")
-    r = subprocess.run(["make", "-C", SAN, "host_check"], capture_output=True, text=True)
+    r = _make("host_check")
     if r.returncode != 0:
         if "asan" in r.stderr.lower() or "sanitize" in r.stderr.lower():
             pytest.skip("toolchain without ASan/UBSan runtime")
@@ -193,7 +202,7 @@ def test_wide_tree_pool_under_tsan():
     threads, each compared byte for byte with the serial build."""
     if not os.path.isdir(SAN) or shutil.which("g++") is None:
         pytest.skip("sanitizer harness not present (GPU box) or no g++")
-    r = subprocess.run(["make", "-C", SAN, "host_check_tsan"], capture_output=True, text=True)
+    r = _make("host_check_tsan")
     if r.returncode != 0:
         if "tsan" in r.stderr.lower() or "sanitize" in r.stderr.lower():
             pytest.skip("toolchain without the TSan runtime")
