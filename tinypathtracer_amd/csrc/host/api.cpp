@@ -1098,7 +1098,13 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // pass, so passes are batched harder there: tir (6 triangles) refill 16
     // 84.6 Grays/s vs 24 72.6-78.9; box (1,932) 16 = 24; C5 (131 K) 16 -3 %.
     const int full = s->n_faces <= 4096 ? 16 : 24;
-    a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 8 : (drained ? 4 : full));
+    // Pair mode (round 3, after the 4-wave pair variants and the fp32-bounded env
+    // lookup; C3 1080p 4096 spp, Mrays/s): refill 8 7,711, 6 7,720, 4 7,790-7,942,
+    // 3 7,911-7,934, 2 7,860-7,983 -> 3; with env IS (the side lane's env sample
+    // and shadow ray per diffuse bounce): 8 5,562-5,630, 4 5,745-5,803, 2
+    // 5,934-5,970, 1 6,070-6,153 -> 1 (the wave shades only once no lane traverses).
+    a.refill = p->refill > 0 ? std::min(p->refill, 64)
+                             : (pair_kernel ? (a.env_is ? 1 : 3) : (drained ? 4 : full));
     a.drained = drained ? 1 : 0;   // latency-oriented kernel variants (trace.hip DRAIN)
     // Parked-leaf batch (speculative leaf postponement): a wave runs its triangle
     // tests once this many lanes are blocked on a parked leaf.  Pair mode has
