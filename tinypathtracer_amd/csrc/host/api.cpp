@@ -1112,7 +1112,10 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // batches less (C3 4096 spp: 4 -> 6.84, 2 -> 7.45, 8 -> 5.86 Grays/s;
     // C2, C4 and C5 within 2 % either way).
     // Drained launches likewise (strong-scaled C2, rank 0 of 8: 4 -> 259 ms, 2 -> 252 ms, 8 -> 277 ms).
-    a.leaf_kb = p->leaf_batch > 0 ? std::min(p->leaf_batch, 64) : ((pair_kernel || drained) ? 2 : 4);
+    // Re-swept at the end of round 3 with the new pair refill (C3: 1 -> 7,988-8,092,
+    // 2 -> 7,826-7,886, 3 -> 7,414-7,457 Mrays/s; C3 + IS: 1 -> 6,191-6,212,
+    // 2 -> 6,111-6,133): 1 in pair mode.
+    a.leaf_kb = p->leaf_batch > 0 ? std::min(p->leaf_batch, 64) : (pair_kernel ? 1 : (drained ? 2 : 4));
     // XCD runs (trace.hip k_trace prologue) for scenes that do not fit one XCD's
     // 4 MiB L2 (≈ 200 B of nodes, triangles and shading data per face): the
     // largest run length <= 10 that divides a row's tiles per XCD (C5 3840 px:
