@@ -258,11 +258,14 @@ def _cpu_model():
     return "unknown"
 
 
-def pmc_summary(args, world, config):
+def pmc_summary(args, world, config, build):
     """The committed rocprofv3 PMC summary of this exact workload (tools/profile.sh
-    writes bench_config into it), or None."""
+    writes bench_config and the profiled library's build identity into it):
+    (path, summary, same_build), preferring one profiled with this very library
+    (same code-object hash); a summary of the same workload from another build
+    is returned flagged (same_build False), or None."""
     import glob
-    best = None
+    best, stale = None, None
     for path in sorted(glob.glob(os.path.join(args.pmc_dir, "*pmc_summary*.json"))):
         try:
             with open(path) as f:
@@ -270,11 +273,14 @@ def pmc_summary(args, world, config):
         except (OSError, ValueError):
             continue
         if pm.get("bench_config") == config and pm.get("n_gpus") == world:
-            best = (path, pm)
-    return best
+            if (pm.get("build") or {}).get("lib_sha256") == build.get("lib_sha256"):
+                best = (path, pm, True)
+            else:
+                stale = (path, pm, False)
+    return best or stale
 
 
-def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_launch_ms):
+def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_launch_ms, build):
     """The trace kernel against the MI355X ceilings.
     Live: algorithmic bytes per step / step time, against the L2-resident gather
     rate.  From the PMC summary of the same workload: per-step VALU
@@ -284,11 +290,12 @@ def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_lau
     limits = {"l2_gather": {"achieved": round(alg, 1), "peak": L2_GATHER_PEAK_GBS, "unit": "GB/s",
                             "frac": round(alg / L2_GATHER_PEAK_GBS, 4), "what": "algorithmic bytes (SURVEY 8(d))"}}
     traffic = None
-    found = pmc_summary(args, world, config)
-    source = None
+    found = pmc_summary(args, world, config, build)
+    source, same_build, pmc_build = None, None, None
     if found:
-        source, pm = found
+        source, pm, same_build = found
         source = os.path.relpath(source, ROOT)
+        pmc_build = pm.get("build")
         c = pm.get("counters_per_launch", {})
         lps = pm.get("launches_per_step") or launches_per_step
         if pm.get("hbm_bytes_per_launch") is not None:
@@ -316,7 +323,9 @@ def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_lau
             "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"], "frac": top["frac"],
             "traffic": traffic, "kernel": "k_trace",
             "bytes_per_step": bytes_step, "launches_per_step": launches_per_step,
-            "avg_launch_ms": round(avg_launch_ms, 3), "limits": limits, "pmc_source": source}
+            "avg_launch_ms": round(avg_launch_ms, 3), "limits": limits, "pmc_source": source,
+            # the PMC summary's library == the one this bench ran (code-object hash)
+            "pmc_same_build": same_build, "pmc_build": pmc_build}
 
 
 KEYS = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hits", "pixels", "samples", "trace_ms",
@@ -497,9 +506,12 @@ def main():
                                       f"pipe_sets={args.pipe_sets}" if args.pipe_sets > 1 else "auto"),
                   "lanes_per_pixel": args.lanes_per_pixel or "auto",
                   "parallelism": par}
-        roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms)
+        build = T.build_identity()
+        roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms, build)
         out = {
-            "metric": "Mrays/s at 1920x1080x1024spp (box.gltf, 8 bounces); achieved GB/s vs peak",
+            # BASELINE.json's metric, naming the workload actually run (C2 by default)
+            "metric": f"Mrays/s at {W}x{H}x{args.spp}spp ({args.scene}.gltf, {args.depth} bounces"
+                      + (", env IS" if args.env_is else "") + "); achieved GB/s vs peak",
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -527,6 +539,7 @@ def main():
                                    "rng_init": round(l_tot["rng_init_ms"] / K, 3),
                                    "trace": round(l_tot["trace_ms"] / K, 3),
                                    "resolve": round(l_tot["resolve_ms"] / K, 3)},
+            "build": build,
             "build_threads": build_threads,
             "async_build": int(args.async_build),
         }

@@ -20,10 +20,10 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _lib
-from ._lib import TPTError, check, lib
+from ._lib import TPTError, build_identity, check, lib
 
 __all__ = ["Camera", "Scene", "DeviceScene", "BVH", "EnvLight", "PathTracer", "Frame", "TPTError",
-           "procedural_sky", "version", "device_count", "NODE_DTYPE"]
+           "procedural_sky", "version", "device_count", "build_identity", "NODE_DTYPE"]
 
 # BVHNode (include/bvh.cuh:52-58): parent, info{left,right | fid,placeHolder}, box
 NODE_DTYPE = np.dtype([("parent", "<u4"), ("a", "<i4"), ("b", "<i4"), ("bmin", "<f4", 3), ("bmax", "<f4", 3)])

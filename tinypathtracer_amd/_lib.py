@@ -118,6 +118,27 @@ class TPTError(RuntimeError):
 _lib = None
 
 
+def build_identity() -> dict:
+    """The library this process runs: the SHA-256 (first 16 hex digits) of
+    libtpt.so's bytes -- its code objects included -- and the git HEAD the
+    Makefile recorded when it linked it (libtpt.build; "-dirty" when the tree
+    had uncommitted changes).  bench.py prints it; tools/pmc_summary.py copies
+    it into every PMC summary, so a bench line can tell whether its counters
+    come from the same build."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    ident = {"lib_sha256": h.hexdigest()[:16], "git_head": None}
+    try:
+        with open(os.path.splitext(LIB_PATH)[0] + ".build") as f:
+            ident["git_head"] = f.read().strip() or None
+    except OSError:
+        pass
+    return ident
+
+
 def lib():
     """Load libtpt.so (fails loudly when the HIP build is missing)."""
     global _lib

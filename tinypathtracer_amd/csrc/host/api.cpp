@@ -109,14 +109,19 @@ struct DeviceGuard {
     }
 };
 
-bool is_device_ptr(const void* p) {
+// *owner (optional): the device that owns a device-memory pointer (-1 for host
+// or managed memory, which every device can address).
+bool is_device_ptr(const void* p, int* owner = nullptr) {
+    if (owner) *owner = -1;
     if (!p) return false;
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
-    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+    const bool dev = attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+    if (attr.type == hipMemoryTypeDevice && owner) *owner = attr.device;
+    return dev;
 }
 
 // A desc array in device memory (the reference's DeviceScene buffers) read back
@@ -467,7 +472,13 @@ tpt_status tpt_scene_create(const tpt_scene_desc* d_in, int device, tpt_scene** 
     dh.materials = host_view(d_in->materials, d_in->n_materials, t_mtl, &herr);
     dh.lights = host_view(d_in->lights, d_in->n_lights, t_lights, &herr);
     if (herr != hipSuccess) return fail(TPT_ERR_HIP, std::string("scene desc readback: ") + hipGetErrorString(herr));
-    const bool verts_dev = is_device_ptr(d_in->vertices), norms_dev = is_device_ptr(d_in->normals);
+    // Device vertices / normals are copied device to device on this scene's
+    // stream, so they must live on `device` itself (another GPU's buffers would
+    // need peer access): a buffer of another device is rejected.
+    int v_owner = -1, n_owner = -1;
+    const bool verts_dev = is_device_ptr(d_in->vertices, &v_owner), norms_dev = is_device_ptr(d_in->normals, &n_owner);
+    if ((v_owner >= 0 && v_owner != device) || (n_owner >= 0 && n_owner != device))
+        return fail(TPT_ERR_INVALID_ARG, "device vertex/normal buffers must live on the scene's device");
 
     for (uint64_t i = 0; i < 3ull * d->n_faces; ++i)
         if (d->indices[i] >= d->n_vertices) return fail(TPT_ERR_INVALID_ARG, "vertex index out of range");
@@ -841,7 +852,7 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
                 s->pending = true;
                 s->built = true;   // (finish_pending completes it)
                 return TPT_OK;
-            } catch (const std::system_error&) {   // no thread: build it here
+            } catch (const std::exception&) {   // no thread (system_error, bad_alloc): build it here
             }
         }
         build_host_trees(j);

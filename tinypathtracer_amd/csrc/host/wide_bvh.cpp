@@ -160,7 +160,10 @@ struct Uninit {
 // are any, so nested waits cannot deadlock, and sleeps otherwise).  Threads are started once per
 // build: on the GPU box starting one costs ≈ 35 µs, 15 at once ≈ 0.6 ms.  A
 // thread that cannot be started (std::system_error under a pid or ulimit cap)
-// just leaves its share to the others; tasks must not throw.
+// just leaves its share to the others.  A task that throws (std::bad_alloc from
+// a split's scratch vectors or a submit) never escapes its thread: the first
+// exception is kept, every counter still moves, and wait_all() / chunks()
+// rethrow it once no task can still reference the waiting frame.
 class Pool {
 public:
     explicit Pool(int threads) {
@@ -181,18 +184,23 @@ public:
         for (auto& t : th_) t.join();
     }
     int threads() const { return 1 + (int)th_.size(); }
+    // Queues f.  Throws (std::bad_alloc) only before anything is counted.
     void submit(std::function<void()> f) {
-        pending_.fetch_add(1, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> g(mu_);
             q_.push_back(std::move(f));
+            pending_.fetch_add(1, std::memory_order_relaxed);   // (under the lock: before any pop)
         }
         cv_.notify_one();
         done_cv_.notify_all();   // a waiter may run it
     }
-    // Runs queued tasks until every submitted task (and what they submit) is done.
-    void wait_all() { help_until(pending_); }
-    // Runs queued tasks until `left` reaches 0.
+    // Runs queued tasks until every submitted task (and what they submit) is
+    // done, then rethrows the first exception a task threw.
+    void wait_all() {
+        help_until(pending_);
+        rethrow();
+    }
+    // Runs queued tasks until `left` reaches 0 (never throws).
     void help_until(const std::atomic<int>& left) {
         while (left.load(std::memory_order_acquire) > 0) {
             if (run_one()) continue;
@@ -200,20 +208,53 @@ public:
             done_cv_.wait(g, [&] { return left.load(std::memory_order_acquire) == 0 || !q_.empty(); });
         }
     }
-    // f(c) for c in [0, nc), chunk 0 on this thread; returns when all are done.
+    // f(c) for c in [0, nc), chunk 0 on this thread; returns when all are done
+    // (rethrowing the first exception of any chunk once none is running).
     template <class F>
     void chunks(int nc, F&& f) {
         std::atomic<int> left{nc - 1};
-        for (int c = 1; c < nc; ++c)
-            submit([&f, &left, c] {
-                f(c);
-                left.fetch_sub(1, std::memory_order_acq_rel);
-            });
-        f(0);
+        int queued = 0;
+        try {
+            for (int c = 1; c < nc; ++c, ++queued)
+                submit([this, &f, &left, c] {
+                    try {
+                        f(c);
+                    } catch (...) {
+                        keep(std::current_exception());
+                    }
+                    left.fetch_sub(1, std::memory_order_acq_rel);
+                });
+            f(0);
+        } catch (...) {
+            keep(std::current_exception());
+        }
+        left.fetch_sub((nc - 1) - queued, std::memory_order_acq_rel);   // chunks never queued
         help_until(left);
+        rethrow();
+    }
+    // Records an exception thrown on this thread by work that shares the pool
+    // (the caller then waits with wait_all(), which rethrows it).
+    void keep(std::exception_ptr e) {
+        std::lock_guard<std::mutex> g(err_mu_);
+        if (!err_) err_ = e;
     }
 
 private:
+    void rethrow() {
+        std::exception_ptr e;
+        {
+            std::lock_guard<std::mutex> g(err_mu_);
+            std::swap(e, err_);
+        }
+        if (e) std::rethrow_exception(e);
+    }
+    void run(std::function<void()>& f) {
+        try {
+            f();
+        } catch (...) {
+            keep(std::current_exception());
+        }
+    }
     bool run_one() {
         std::function<void()> f;
         {
@@ -222,7 +263,7 @@ private:
             f = std::move(q_.front());
             q_.pop_front();
         }
-        f();
+        run(f);
         finished();
         return true;
     }
@@ -243,7 +284,7 @@ private:
                 f = std::move(q_.front());
                 q_.pop_front();
             }
-            f();
+            run(f);
             finished();
         }
     }
@@ -254,6 +295,8 @@ private:
     std::deque<std::function<void()>> q_;
     std::atomic<int> pending_{0};
     bool stop_ = false;
+    std::mutex err_mu_;
+    std::exception_ptr err_;
 };
 
 #ifndef TPT_WIDE_BINS
@@ -750,8 +793,12 @@ int build_wide_sah(const std::vector<int>& pos, const float* leaf_box, const uin
     const int root = 0;
     mark("setup");
     if (n >= Builder::kTask) {
-        B.build_task(0, n, root, leaf_emit, cb, 0);
-        pool.wait_all();
+        try {
+            B.build_task(0, n, root, leaf_emit, cb, 0);
+        } catch (...) {   // tasks it queued may still run: they reference B
+            pool.keep(std::current_exception());
+        }
+        pool.wait_all();   // (rethrows once no task is left)
         std::sort(B.upper.begin(), B.upper.end(), std::greater<int>());
         for (int id : B.upper) B.finish(id, B.nodes[id].left, B.nodes[id].right);
     } else {

@@ -886,6 +886,12 @@ struct PathRecords {
     __device__ __forceinline__ float get(int level, int w) const {
         return level < nlds ? lds[(level * words + w) * RS] : deep[level * 5 + w];
     }
+    // word w of a level known to live in LDS (level < nlds), for records of
+    // WORDS words per level (the caller's variant fixes it)
+    template <int WORDS>
+    __device__ __forceinline__ float lds_at(int level, int w) const {
+        return lds[(level * WORDS + w) * RS];
+    }
     // mk = material id | p-kind << 30; probe = material the probe hit (kNoProbe: none).
     // Pair mode (5 words, PACKED_PROBE): w1 = mk | probe << 15 as in the 2-word
     // records and w2..w4 = the delta lights' direct sum alone, written by whichever
@@ -1315,14 +1321,15 @@ void k_trace(TraceArgs a) {
                 // DRAIN variants: every level's record and materials read before the
                 // arithmetic, so the unwind pays one LDS latency chain instead of one
                 // per level (the same operations in the same order as below)
+                static_assert(!PAIR && !LIGHTS, "DRAIN unwind: one-lane 2-word records");
                 if (finish && rec.nlds >= 8) {
                     unwound = true;
                     float af[8];
                     uint32_t w1[8];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
-                        af[k] = rec.lds[(2 * k) * 256];
-                        w1[k] = k < depth ? __float_as_uint(rec.lds[(2 * k + 1) * 256]) : (kNoProbe << 15);
+                        af[k] = rec.template lds_at<2>(k, 0);
+                        w1[k] = k < depth ? __float_as_uint(rec.template lds_at<2>(k, 1)) : (kNoProbe << 15);
                     }
                     float4 mb[8];
                     float ee[8];

@@ -89,6 +89,7 @@ try:
                 s["bench_value"] = b.get("value")
                 s["bench_ms_per_step"] = b.get("ms_per_step")
                 s["launches_per_step"] = b.get("roofline", {}).get("launches_per_step")
+                s["build"] = b.get("build")   # the profiled library: code-object hash + git HEAD
 except OSError:
     pass
 print(json.dumps(s, indent=1))
