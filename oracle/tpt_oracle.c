@@ -625,39 +625,67 @@ static inline v3 env_lookup(const orc_env* env, v3 d, int tm) {
 }
 
 /* Env importance sampling: the build's A15 re-derivation (env_light.cu:10-54
- * intends a 2-D piecewise-constant distribution).  Weight =
- * luma * sin(theta at the row centre), rows iy = 0 (bottom) .. h-1 as the
- * lookup reads them, all sums sequential in float. */
+ * intends a 2-D piecewise-constant distribution), restating
+ * libtpt's format (api.cpp build_env_is, trace.hip env_is_sample): piecewise
+ * constant over blocks of B x B texels, B = 1 up to 2^17 texels and doubled
+ * until the block grid has at most 2^17 cells.  Block weight = sum over its
+ * texels (texel rows, then columns) of luma * sin(theta at the texel row's
+ * centre), rows iy = 0 (bottom) .. h-1 as the lookup reads them; sequential
+ * float prefix sums per block row and over block rows. */
 typedef struct {
-    float *w, *cond, *row, *marg;
+    float *cond, *row, *marg;
     float total;
+    int b, bw, bh;
 } env_is_t;
+
+static int env_is_block(int w, int h) {
+    int b = 1;
+    while ((long long)((w + b - 1) / b) * (long long)((h + b - 1) / b) > (1ll << 17)) b *= 2;
+    return b;
+}
+
+static void env_is_free(env_is_t* t) {
+    free(t->cond);
+    free(t->row);
+    free(t->marg);
+}
 
 static void env_is_build(const orc_env* env, env_is_t* t) {
     const int w = env->w, h = env->h;
-    t->w = (float*)malloc(sizeof(float) * (size_t)w * h);
-    t->cond = (float*)malloc(sizeof(float) * (size_t)w * h);
-    t->row = (float*)malloc(sizeof(float) * (size_t)h);
-    t->marg = (float*)malloc(sizeof(float) * (size_t)h);
-    float acc_rows = 0.0f;
+    const int b = env_is_block(w, h), bw = (w + b - 1) / b, bh = (h + b - 1) / b;
+    t->b = b;
+    t->bw = bw;
+    t->bh = bh;
+    t->cond = (float*)malloc(sizeof(float) * (size_t)bw * bh);
+    t->row = (float*)malloc(sizeof(float) * (size_t)bh);
+    t->marg = (float*)malloc(sizeof(float) * (size_t)bh);
+    float* sw = (float*)malloc(sizeof(float) * (size_t)h);
     for (int iy = 0; iy < h; ++iy) {
         const float theta = PI_F * (1.0f - ((float)iy + 0.5f) / (float)h);
-        float sw, cw;
-        parity_sincos(theta, &sw, &cw);
+        float cw;
+        parity_sincos(theta, &sw[iy], &cw);
+    }
+    float acc_rows = 0.0f;
+    for (int by = 0; by < bh; ++by) {
         float acc = 0.0f;
-        for (int ix = 0; ix < w; ++ix) {
-            const uint8_t* px = env->rgba + 4 * ((size_t)iy * w + ix);
-            const float luma = (0.2126f * (float)px[0] + 0.7152f * (float)px[1]) + 0.0722f * (float)px[2];
-            const float wt = luma * sw;
-            t->w[(size_t)iy * w + ix] = wt;
-            acc = acc + wt;
-            t->cond[(size_t)iy * w + ix] = acc;
+        for (int bx = 0; bx < bw; ++bx) {
+            float wb = 0.0f;
+            const int ye = by * b + b < h ? by * b + b : h, xe = bx * b + b < w ? bx * b + b : w;
+            for (int iy = by * b; iy < ye; ++iy)
+                for (int ix = bx * b; ix < xe; ++ix) {
+                    const uint8_t* px = env->rgba + 4 * ((size_t)iy * w + ix);
+                    const float luma = (0.2126f * (float)px[0] + 0.7152f * (float)px[1]) + 0.0722f * (float)px[2];
+                    wb = wb + luma * sw[iy];
+                }
+            acc = acc + wb;
+            t->cond[(size_t)by * bw + bx] = acc;
         }
-        t->row[iy] = acc;
+        t->row[by] = acc;
         acc_rows = acc_rows + acc;
-        t->marg[iy] = acc_rows;
+        t->marg[by] = acc_rows;
     }
     t->total = acc_rows;
+    free(sw);
 }
 
 static int lower_bound_f(const float* a, int n, float t) {
@@ -669,31 +697,38 @@ static int lower_bound_f(const float* a, int n, float t) {
     return lo;
 }
 
-/* One env sample for a diffuse hit with incident-side normal nf: direction and
- * the contribution factor Le * cos / (pi * pdf); 0 when it cannot contribute
- * (the two uniforms are drawn either way). */
+/* One env sample for a diffuse hit with incident-side normal nf: a block by
+ * the two CDFs, a point uniformly inside it, the direction and the
+ * contribution factor Le * cos / (pi * pdf) with pdf = (p_block * W * H /
+ * block texels) / (2 pi^2 sin(theta)), p_block from the CDF steps; 0 when it
+ * cannot contribute (the two uniforms are drawn either way). */
 static int env_is_sample(const orc_env* env, const env_is_t* t, v3 nf, uint32_t st[6], int tm, v3* dir, v3* k_le) {
     const float x1 = orc_uniform(st);
     const float x2 = orc_uniform(st);
-    const int W = env->w, H = env->h;
+    const int W = env->w, H = env->h, B = t->b, BW = t->bw, BH = t->bh;
     const float t1 = x1 * t->total;
-    const int iy = lower_bound_f(t->marg, H, t1);
-    const float lo1 = iy > 0 ? t->marg[iy - 1] : 0.0f;
-    const float f1 = fminf((t1 - lo1) / (t->marg[iy] - lo1), 0.99999994f);
-    const float* cond = t->cond + (size_t)iy * W;
-    const float t2 = x2 * t->row[iy];
-    const int ix = lower_bound_f(cond, W, t2);
-    const float lo2 = ix > 0 ? cond[ix - 1] : 0.0f;
-    const float f2 = fminf((t2 - lo2) / (cond[ix] - lo2), 0.99999994f);
-    const float u = ((float)ix + f2) / (float)W;
-    const float v = ((float)iy + f1) / (float)H;
+    const int by = lower_bound_f(t->marg, BH, t1);
+    const float lo1 = by > 0 ? t->marg[by - 1] : 0.0f;
+    const float hi1 = t->marg[by];
+    const float f1 = fminf((t1 - lo1) / (hi1 - lo1), 0.99999994f);
+    const float* cond = t->cond + (size_t)by * BW;
+    const float rs = t->row[by];
+    const float t2 = x2 * rs;
+    const int bx = lower_bound_f(cond, BW, t2);
+    const float lo2 = bx > 0 ? cond[bx - 1] : 0.0f;
+    const float hi2 = cond[bx];
+    const float f2 = fminf((t2 - lo2) / (hi2 - lo2), 0.99999994f);
+    const int x0 = bx * B, y0 = by * B;
+    const int wb = B < W - x0 ? B : W - x0, hb = B < H - y0 ? B : H - y0;
+    const float u = ((float)x0 + f2 * (float)wb) / (float)W;
+    const float v = ((float)y0 + f1 * (float)hb) / (float)H;
     float sp, cp, sth, cth;
     parity_sincos((2.0f * PI_F) * u, &sp, &cp);
     parity_sincos(PI_F * (1.0f - v), &sth, &cth);
     *dir = V3(sth * cp, cth, sth * sp);
     const float c = vdot(*dir, nf);
-    const float pdf = ((t->w[(size_t)iy * W + ix] / t->total) * ((float)W * (float)H)) /
-                      ((2.0f * PI_F * PI_F) * sth);
+    const float pb = ((hi2 - lo2) / rs) * ((hi1 - lo1) / t->total);
+    const float pdf = (pb * (((float)W * (float)H) / (float)(wb * hb))) / ((2.0f * PI_F * PI_F) * sth);
     if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < 3.40282347e+38f)) return 0;
     const v3 le = env_lookup(env, *dir, tm);
     const float k = c / (PI_F * pdf);
@@ -708,7 +743,7 @@ int orc_env_is_samples(const uint8_t* rgba, int w, int h, const float nf[3], uin
     orc_env env = {rgba, w, h};
     env_is_t t;
     env_is_build(&env, &t);
-    if (!(t.total > 0.0f)) { free(t.w); free(t.cond); free(t.row); free(t.marg); return -1; }
+    if (!(t.total > 0.0f)) { env_is_free(&t); return -1; }
     orc_xorwow_jump_matrices();
     uint32_t st[6];
     orc_xorwow_init(seed, 0, st);
@@ -718,7 +753,7 @@ int orc_env_is_samples(const uint8_t* rgba, int w, int h, const float nf[3], uin
         dirs[3 * i] = d.x; dirs[3 * i + 1] = d.y; dirs[3 * i + 2] = d.z;
         k_le[3 * i] = k.x; k_le[3 * i + 1] = k.y; k_le[3 * i + 2] = k.z;
     }
-    free(t.w); free(t.cond); free(t.row); free(t.marg);
+    env_is_free(&t);
     return 0;
 }
 
@@ -892,7 +927,7 @@ int orc_render(const orc_scene* s, const orc_env* env, const orc_camera* cam, co
     c.s = s; c.env = env; c.c2w = cam->c2w; c.vfov = cam->vfov; c.aspect = cam->aspect;
     c.W = W; c.H = H; c.spp = p->spp; c.max_depth = p->max_depth; c.tm = p->trig_mode;
     c.tan_half = t_tan(p->trig_mode, cam->vfov * 0.5f);
-    env_is_t is_tab = {NULL, NULL, NULL, NULL, 0.0f};
+    env_is_t is_tab = {NULL, NULL, NULL, 0.0f, 1, 0, 0};
     c.is = NULL;
     if (p->env_is && env && env->rgba) {
         env_is_build(env, &is_tab);
@@ -948,7 +983,7 @@ int orc_render(const orc_scene* s, const orc_env* env, const orc_camera* cam, co
         out->init_ms = t1 - t0; out->trace_ms = t2 - t1;
     }
     free(wv); free(wn); free(nodes); free(keys); free(states);
-    free(is_tab.w); free(is_tab.cond); free(is_tab.row); free(is_tab.marg);
+    env_is_free(&is_tab);
     return 0;
 }
 

@@ -60,14 +60,15 @@ struct TraceArgs {
     // env (nullable)
     const uint32_t* env;                 // RGBA8 packed, row 0 = bottom
     int32_t env_w, env_h;
-    const float* is_w;                   // env importance sampling (A15): texel weights [h][w]
-    const float* is_cond;                //   row prefix sums [h][w]
-    const float* is_row;                 //   row sums [h]
-    const float* is_marg;                //   marginal prefix over rows [h]
+    // env importance sampling (A15) over blocks of is_b x is_b texels (api.cpp build_env_is)
+    int32_t is_b, is_bw, is_bh;          // block side; blocks per block row; block rows
+    const float* is_cond;                //   block-row prefix sums [bh][bw]
+    const float* is_row;                 //   block-row sums [bh]
+    const float* is_marg;                //   marginal prefix over block rows [bh]
     float is_total;
     // guide tables of the two searches (exact lower_bound in few dependent loads):
     // is_guide_r[k] = lower_bound(is_marg, (k / kr) * is_total), k = 0..kr;
-    // is_guide_c[iy * (kc + 1) + k] = lower_bound(row iy of is_cond, (k / kc) * is_row[iy])
+    // is_guide_c[by * (kc + 1) + k] = lower_bound(block row by of is_cond, (k / kc) * is_row[by])
     const int32_t* is_guide_r;
     const int32_t* is_guide_c;
     int32_t is_kr, is_kc;                // powers of two
@@ -91,6 +92,12 @@ struct TraceArgs {
     int32_t any_emitter;                 // some triangle emits (else a direct probe adds nothing)
     int32_t emit_root;                   // inner4 id of the emissive-triangle tree (-1: none)
     int32_t emit_inline;                 // that tree is one node of leaves: probe pass 1 in the shading pass
+    // Boxes enclosing every emissive triangle's leaf box (the emissive tree
+    // root's child boxes, overlapping ones merged): (lo.xyz, 0), (hi.xyz, 0) per
+    // box.  A direct probe whose line misses all of them by a margin can hit no
+    // emitter and is resolved in the shading pass (trace.hip probe_misses_emitters)
+    float4 emit_box[8];
+    int32_t n_emit_box;                  // 0: no pre-test (no emissive tree, or non-finite boxes)
     const float4* sliver_groups;         // 2 per group: (lo.xyz, first), (hi.xyz, count) (trace.hip "Culling")
     const float4* sliver_list;           // 2 per sliver: (exact leaf box lo.xyz, position | emissive << 30), (hi.xyz, 0)
     int32_t n_sliver_groups;             // 0: no sliver triangles

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <memory>
 #include <new>
 #include <string>
@@ -164,10 +165,12 @@ struct tpt_env {
     int device = 0;
     int w = 0, h = 0;
     DevBuf<uint32_t> texels;
-    // importance-sampling tables (A15, TPT_FLAG_ENV_IS): per-texel weight, row
-    // prefix sums, row sums, marginal prefix over rows; total <= 0 disables
-    DevBuf<float> is_w, is_cond, is_row, is_marg;
+    // importance-sampling tables (A15, TPT_FLAG_ENV_IS) over blocks of B x B
+    // texels: block-row prefix sums, block-row sums, marginal prefix over block
+    // rows; total <= 0 disables
+    DevBuf<float> is_cond, is_row, is_marg;
     float is_total = 0.0f;
+    int32_t is_b = 1, is_bw = 0, is_bh = 0;   // block side, blocks per row, block rows
     DevBuf<int32_t> is_guide_r, is_guide_c;   // guide tables of the two CDF searches (trace.hip lower_bound_guided)
     int32_t is_kr = 1, is_kc = 1;
 };
@@ -176,33 +179,50 @@ namespace {
 
 // A15 re-derivation (env_light.cu:10-54 intends a 2-D piecewise-constant
 // distribution; its weight uses theta for sin(theta), its normalisation races
-// across blocks and its row orientation is the reverse of Vec2UV).  Here:
-// w = luma * sin(theta at the row centre), rows iy = 0 (bottom) .. h-1 as the
-// lookup reads them (v = 1 - acos(y)/pi), all sums sequential in float --
-// the oracle builds the same tables with the same operations.
-void build_env_is(const uint8_t* rgba, int w, int h, std::vector<float>& W, std::vector<float>& cond,
-                  std::vector<float>& row, std::vector<float>& marg, float& total) {
-    W.resize((size_t)w * h);
-    cond.resize((size_t)w * h);
-    row.resize(h);
-    marg.resize(h);
-    float acc_rows = 0.0f;
+// across blocks and its row orientation is the reverse of Vec2UV).  Here the
+// distribution is piecewise constant over blocks of B x B texels (B = 1 for
+// maps up to 2^17 texels; doubled until the block grid has at most 2^17 cells,
+// so the tables stay L2-resident: 2048 x 1024 -> B = 4, 512 x 256 blocks,
+// 0.5 MB): a block's weight is the sum over its texels of luma * sin(theta at
+// the texel row's centre), rows iy = 0 (bottom) .. h-1 as the lookup reads them
+// (v = 1 - acos(y)/pi), texel rows then columns, then sequential float prefix
+// sums per block row and over block rows -- the oracle (env_is_build) builds
+// the same tables with the same operations.  A sample picks a block by the two
+// CDFs and a point uniformly inside it (trace.hip env_is_sample).
+int env_is_block(int w, int h) {
+    int b = 1;
+    while ((long long)((w + b - 1) / b) * (long long)((h + b - 1) / b) > (1ll << 17)) b *= 2;
+    return b;
+}
+void build_env_is(const uint8_t* rgba, int w, int h, int b, std::vector<float>& cond, std::vector<float>& row,
+                  std::vector<float>& marg, float& total) {
+    const int bw = (w + b - 1) / b, bh = (h + b - 1) / b;
+    cond.resize((size_t)bw * bh);
+    row.resize(bh);
+    marg.resize(bh);
+    std::vector<float> sw(h);
     for (int iy = 0; iy < h; ++iy) {
         const float theta = tpt::kPi * (1.0f - ((float)iy + 0.5f) / (float)h);
-        float sw, cw;
-        tpt::fsincos_2pi(theta, sw, cw);
+        float cw;
+        tpt::fsincos_2pi(theta, sw[iy], cw);
+    }
+    float acc_rows = 0.0f;
+    for (int by = 0; by < bh; ++by) {
         float acc = 0.0f;
-        for (int ix = 0; ix < w; ++ix) {
-            const uint8_t* px = rgba + 4 * ((size_t)iy * w + ix);
-            const float luma = (0.2126f * (float)px[0] + 0.7152f * (float)px[1]) + 0.0722f * (float)px[2];
-            const float wt = luma * sw;
-            W[(size_t)iy * w + ix] = wt;
-            acc = acc + wt;
-            cond[(size_t)iy * w + ix] = acc;
+        for (int bx = 0; bx < bw; ++bx) {
+            float wb = 0.0f;
+            for (int iy = by * b; iy < std::min(by * b + b, h); ++iy)
+                for (int ix = bx * b; ix < std::min(bx * b + b, w); ++ix) {
+                    const uint8_t* px = rgba + 4 * ((size_t)iy * w + ix);
+                    const float luma = (0.2126f * (float)px[0] + 0.7152f * (float)px[1]) + 0.0722f * (float)px[2];
+                    wb = wb + luma * sw[iy];
+                }
+            acc = acc + wb;
+            cond[(size_t)by * bw + bx] = acc;
         }
-        row[iy] = acc;
+        row[by] = acc;
         acc_rows = acc_rows + acc;
-        marg[iy] = acc_rows;
+        marg[by] = acc_rows;
     }
     total = acc_rows;
 }
@@ -334,6 +354,8 @@ struct tpt_scene {
     int32_t wide_tree = 0;                  // 1: inner4 holds the SAH 4-wide tree (wide_bvh.cpp)
     int32_t emit_root = -1;                 // inner4 id of the emissive-triangle tree's root (-1: none)
     int32_t emit_inline = 0;                // that tree is one node of leaves (<= 4 emitters)
+    float emit_box[24] = {};                // boxes around the emitters' leaf boxes (TraceArgs emit_box)
+    int32_t n_emit_box = 0;
     int32_t slivers = 0;                    // sliver triangles (trace.hip "Culling"), re-tested after traversal
     int32_t n_sliver_groups = 0;
     DevBuf<float4> sliver_groups, sliver_list;
@@ -579,6 +601,51 @@ tpt_status tpt_scene_set_build_threads(tpt_scene* s, int32_t threads) {
 
 namespace {
 
+// The direct-probe pre-test's boxes (trace.hip probe_misses_emitters): the
+// child boxes of the emissive tree's root node (4-wide layout, wide_bvh.cpp;
+// they enclose every emissive triangle's leaf box), with a pair merged into
+// its union while the union's surface area is at most the pair's summed areas
+// (heavily overlapping boxes, e.g. the two triangles of one quad light, cost
+// a test each for nothing).  Writes lo.xyz, hi.xyz per box and returns the box
+// count (0: a non-finite box, no pre-test).
+float box_area(const float* b) {
+    const float x = b[3] - b[0], y = b[4] - b[1], z = b[5] - b[2];
+    return 2.0f * (x * y + y * z + z * x);
+}
+int emitter_boxes(const float* root, float* out) {
+    float bx[4][6];
+    int n = 0;
+    int32_t links[4];
+    std::memcpy(links, root + 24, sizeof links);
+    for (int k = 0; k < 4; ++k) {
+        if (links[k] < 0) continue;
+        for (int i = 0; i < 6; ++i) {
+            if (!std::isfinite(root[6 * k + i])) return 0;
+            bx[n][i] = root[6 * k + i];
+        }
+        ++n;
+    }
+    for (bool merged = true; merged && n > 1;) {
+        merged = false;
+        for (int a = 0; a < n && !merged; ++a)
+            for (int b = a + 1; b < n && !merged; ++b) {
+                float u[6];
+                for (int i = 0; i < 3; ++i) {
+                    u[i] = std::min(bx[a][i], bx[b][i]);
+                    u[3 + i] = std::max(bx[a][3 + i], bx[b][3 + i]);
+                }
+                if (box_area(u) <= box_area(bx[a]) + box_area(bx[b])) {
+                    std::memcpy(bx[a], u, sizeof u);
+                    std::memcpy(bx[b], bx[n - 1], sizeof u);
+                    --n;
+                    merged = true;
+                }
+            }
+    }
+    for (int k = 0; k < n; ++k) std::memcpy(out + 6 * k, bx[k], sizeof bx[k]);
+    return n;
+}
+
 // Uploads a finished HostTrees job and completes the scene (the stack bound).
 tpt_status upload_host_trees(tpt_scene* s, HostTrees& j, uint32_t* wide_need) {
     if (j.st != TPT_OK) return fail(j.st, j.msg);
@@ -594,6 +661,7 @@ tpt_status upload_host_trees(tpt_scene* s, HostTrees& j, uint32_t* wide_need) {
                                    hipMemcpyHostToDevice, s->stream));
         s->emit_root = s->n4;
         s->emit_inline = j.ne4 == 1 ? 1 : 0;
+        s->n_emit_box = emitter_boxes(j.e4.data(), s->emit_box);
         *wide_need = std::max(*wide_need, (uint32_t)j.eneed);
     }
     HIP_OR_FAIL(hipStreamSynchronize(s->stream));   // (the host buffers are freed after this)
@@ -720,6 +788,7 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
     s->wide_tree = 0;
     s->emit_root = -1;
     s->emit_inline = 0;
+    s->n_emit_box = 0;
     s->slivers = 0;
     s->n_sliver_groups = 0;
     s->cull_eps = 0.0f;
@@ -883,19 +952,23 @@ tpt_status tpt_env_create(const uint8_t* rgba, int32_t w, int32_t h, int device,
     env->h = h;
     hipError_t e = env->texels.alloc((size_t)w * (size_t)h);
     if (e == hipSuccess) e = hipMemcpy(env->texels.p, rgba, (size_t)w * h * 4, hipMemcpyHostToDevice);
-    std::vector<float> iw, icond, irow, imarg;
-    build_env_is(rgba, w, h, iw, icond, irow, imarg, env->is_total);
-    if (e == hipSuccess) e = env->is_w.upload(iw.data(), iw.size(), nullptr);
+    std::vector<float> icond, irow, imarg;
+    env->is_b = env_is_block(w, h);
+    env->is_bw = (w + env->is_b - 1) / env->is_b;
+    env->is_bh = (h + env->is_b - 1) / env->is_b;
+    const int bw = env->is_bw, bh = env->is_bh;
+    build_env_is(rgba, w, h, env->is_b, icond, irow, imarg, env->is_total);
     if (e == hipSuccess) e = env->is_cond.upload(icond.data(), icond.size(), nullptr);
     if (e == hipSuccess) e = env->is_row.upload(irow.data(), irow.size(), nullptr);
     if (e == hipSuccess) e = env->is_marg.upload(imarg.data(), imarg.size(), nullptr);
-    {   // guide tables: rows at the row count, columns at a quarter of the row length
-        env->is_kr = pow2_at_least(h);
-        env->is_kc = pow2_at_least(std::max(1, w / 4));
-        std::vector<int32_t> gr((size_t)env->is_kr + 1), gc((size_t)h * (env->is_kc + 1));
-        build_guide(imarg.data(), h, env->is_total, env->is_kr, gr.data());
-        for (int iy = 0; iy < h; ++iy)
-            build_guide(icond.data() + (size_t)iy * w, w, irow[iy], env->is_kc, gc.data() + (size_t)iy * (env->is_kc + 1));
+    {   // guide tables: block rows at the block-row count, columns at a quarter of a block row
+        env->is_kr = pow2_at_least(bh);
+        env->is_kc = pow2_at_least(std::max(1, bw / 4));
+        std::vector<int32_t> gr((size_t)env->is_kr + 1), gc((size_t)bh * (env->is_kc + 1));
+        build_guide(imarg.data(), bh, env->is_total, env->is_kr, gr.data());
+        for (int by = 0; by < bh; ++by)
+            build_guide(icond.data() + (size_t)by * bw, bw, irow[by], env->is_kc,
+                        gc.data() + (size_t)by * (env->is_kc + 1));
         if (e == hipSuccess) e = env->is_guide_r.upload(gr.data(), gr.size(), nullptr);
         if (e == hipSuccess) e = env->is_guide_c.upload(gc.data(), gc.size(), nullptr);
     }
@@ -964,6 +1037,15 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.boxes_finite = s->boxes_finite;
     a.any_emitter = s->any_emitter;
     a.emit_root = s->emit_root;
+    a.n_emit_box = s->any_emitter ? s->n_emit_box : 0;
+    for (int k = 0; k < a.n_emit_box; ++k) {
+        const float* b = s->emit_box + 6 * k;
+        a.emit_box[2 * k] = make_float4(b[0], b[1], b[2], 0.0f);
+        a.emit_box[2 * k + 1] = make_float4(b[3], b[4], b[5], 0.0f);
+    }
+#ifdef TPT_NO_PROBE_PRETEST
+    a.n_emit_box = 0;   // A/B builds: no probe pre-test
+#endif
     a.sliver_groups = s->sliver_groups.p;
     a.sliver_list = s->sliver_list.p;
     a.n_sliver_groups = s->n_sliver_groups;
@@ -977,7 +1059,9 @@ static tpt_status fill_trace_args(tpt_scene* s, const tpt_env* env, const tpt_ca
     a.env = env ? env->texels.p : nullptr;
     a.env_w = env ? env->w : 0;
     a.env_h = env ? env->h : 0;
-    a.is_w = env ? env->is_w.p : nullptr;
+    a.is_b = env ? env->is_b : 1;
+    a.is_bw = env ? env->is_bw : 0;
+    a.is_bh = env ? env->is_bh : 0;
     a.is_cond = env ? env->is_cond.p : nullptr;
     a.is_row = env ? env->is_row.p : nullptr;
     a.is_marg = env ? env->is_marg.p : nullptr;

@@ -72,6 +72,13 @@
 #ifndef TPT_ENV_FAST
 #define TPT_ENV_FAST 1     // env texel indices from fp32 bounds, double trig only near texel edges (0: A/B builds)
 #endif
+#ifndef TPT_PROBE_INLINE
+// 1: probe pass 1 inside the shading pass for <= 4 emitters (INL variants,
+// emit_probe_inline; round 3).  0 (default): the bounding-sphere pre-test
+// (probe_misses_emitters) resolves the probes that can hit no emitter in the
+// shading pass and the others trace pass 1 as a traversal.
+#define TPT_PROBE_INLINE 0
+#endif
 #ifndef TPT_ENV_INLINE
 #define TPT_ENV_INLINE 0   // 1: env_lookup inlined in every variant (A/B builds)
 #endif
@@ -529,6 +536,36 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
     }
 }
 
+// Direct-probe pre-test (path_tracer.cu:382-405; DESIGN.md section 5 "Probe
+// pre-test").  The probe only adds the emission of its closest hit, and an
+// emissive triangle can be that hit only if the probe's line passes its leaf
+// box (rayHitBBox, :61-107), which lies inside one of the boxes a.emit_box
+// (api.cpp emitter_boxes).  This is the slab test of those boxes with the
+// hardware's approximate reciprocal (v_rcp_f32, 1 ulp) instead of the
+// correctly rounded 1/d, and it answers "miss" only when the slab intervals
+// fail to overlap by more than 2^-16 (|T0| + |T1|).  Every t it computes is
+// within ~2^-21 relative of the exact (n - o) / d, and so is every t of the
+// reference's float test (1/d rounded, then two roundings); the max/min over
+// axes keeps that bound relative to |T0|, |T1| themselves, and an enclosing
+// box's interval contains a leaf box's (a factor 2 on the |T| sum at most):
+// a line whose leaf box the reference enters always fails this miss test, with
+// a 30x margin.  A probe that misses every box has no emitter hit -- exactly
+// the traversal's "no hit" of pass 1 (kNoProbe), whatever path or culls the
+// traversal would take.  Non-finite reciprocals or products: traced.
+__device__ __forceinline__ bool probe_misses_emitters(const TraceArgs& a, V3 o, V3 d) {
+    if (a.n_emit_box <= 0) return false;
+    const V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    bool miss = __builtin_isfinite(inv.x) & __builtin_isfinite(inv.y) & __builtin_isfinite(inv.z) &
+                __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z);
+    for (int k = 0; k < a.n_emit_box; ++k) {   // (uniform trip count)
+        const float4 lo = a.emit_box[2 * k], hi = a.emit_box[2 * k + 1];
+        float t0, t1;
+        slab_minmax(o, inv, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, t0, t1);
+        miss = miss & ((t0 - t1) > 0x1p-16f * (fabs_(t0) + fabs_(t1)));
+    }
+    return miss;
+}
+
 // Slivers (Culling): the triangles the culled traversal cannot be trusted to
 // reach when they matter, re-tested after it against their exact leaf boxes.
 // Group g: sliver_groups[2g] = (lo.xyz, first), [2g + 1] = (hi.xyz, count)
@@ -768,27 +805,39 @@ __device__ __forceinline__ int lower_bound_guided(const float* __restrict__ a, i
 }
 
 // x1, x2: the two uniforms, drawn by the pixel's path lane in RNG order (pair
-// mode hands them to the side lane with the bounce's shadow job).
+// mode hands them to the side lane with the bounce's shadow job).  The
+// distribution is piecewise constant over blocks of B x B texels (api.cpp
+// build_env_is): a block row by the marginal CDF, a block by that row's CDF,
+// the remapped uniforms as the position inside the block (x0 + f2 * width,
+// y0 + f1 * height in texels), and the pdf from the CDF steps the two
+// searches stood on (the block's probability; no per-texel weight table, so
+// the tables are 0.5 MB for a 2048 x 1024 map -- L2-resident):
+// pdf = (p_block * W * H / (block texels)) / (2 pi^2 sin(theta)).
 __device__ __forceinline__ bool env_is_sample(const TraceArgs& a, V3 nf, float x1, float x2, V3& dir, V3& k_le) {
-    const int W = a.env_w, H = a.env_h;
+    const int W = a.env_w, H = a.env_h, B = a.is_b, BW = a.is_bw, BH = a.is_bh;
     const float t1 = x1 * a.is_total;
-    const int iy = lower_bound_guided(a.is_marg, H, t1, x1, a.is_guide_r, a.is_kr);
-    const float lo1 = iy > 0 ? a.is_marg[iy - 1] : 0.0f;
-    const float f1 = fminf((t1 - lo1) / (a.is_marg[iy] - lo1), 0.99999994f);
-    const float* cond = a.is_cond + (size_t)iy * (size_t)W;
-    const float t2 = x2 * a.is_row[iy];
-    const int ix = lower_bound_guided(cond, W, t2, x2, a.is_guide_c + (size_t)iy * (size_t)(a.is_kc + 1), a.is_kc);
-    const float lo2 = ix > 0 ? cond[ix - 1] : 0.0f;
-    const float f2 = fminf((t2 - lo2) / (cond[ix] - lo2), 0.99999994f);
-    const float u = ((float)ix + f2) / (float)W;
-    const float v = ((float)iy + f1) / (float)H;
+    const int by = lower_bound_guided(a.is_marg, BH, t1, x1, a.is_guide_r, a.is_kr);
+    const float lo1 = by > 0 ? a.is_marg[by - 1] : 0.0f;
+    const float hi1 = a.is_marg[by];
+    const float f1 = fminf((t1 - lo1) / (hi1 - lo1), 0.99999994f);
+    const float* cond = a.is_cond + (size_t)by * (size_t)BW;
+    const float rs = a.is_row[by];
+    const float t2 = x2 * rs;
+    const int bx = lower_bound_guided(cond, BW, t2, x2, a.is_guide_c + (size_t)by * (size_t)(a.is_kc + 1), a.is_kc);
+    const float lo2 = bx > 0 ? cond[bx - 1] : 0.0f;
+    const float hi2 = cond[bx];
+    const float f2 = fminf((t2 - lo2) / (hi2 - lo2), 0.99999994f);
+    const int x0 = bx * B, y0 = by * B;
+    const int wb = min(B, W - x0), hb = min(B, H - y0);
+    const float u = ((float)x0 + f2 * (float)wb) / (float)W;
+    const float v = ((float)y0 + f1 * (float)hb) / (float)H;
     float sp, cp, sth, cth;
     fsincos_2pi((2.0f * kPi) * u, sp, cp);
     fsincos_2pi(kPi * (1.0f - v), sth, cth);
     dir = v3(sth * cp, cth, sth * sp);
     const float c = dot(dir, nf);
-    const float pdf = ((a.is_w[(size_t)iy * (size_t)W + ix] / a.is_total) * ((float)W * (float)H)) /
-                      ((2.0f * kPi * kPi) * sth);
+    const float pb = ((hi2 - lo2) / rs) * ((hi1 - lo1) / a.is_total);
+    const float pdf = (pb * (((float)W * (float)H) / (float)(wb * hb))) / ((2.0f * kPi * kPi) * sth);
     if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < kRealMax)) return false;
     const V3 le = env_lookup<true>(a.env, W, H, dir);
     const float k = c / (kPi * pdf);
@@ -1253,16 +1302,18 @@ void k_trace(TraceArgs a) {
                     } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
                         float af2;
                         new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
-                        tg = grazing(gpass, td);
-                        if (TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) {
-                            // no triangle emits: the probe's emitter pass ends at the
-                            // root with no hit, exactly as a traversal would (the ray
-                            // is still counted: the reference traces it)
+                        if ((TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) ||
+                            (ORDERED && probe_misses_emitters(a, r.o, td))) {
+                            // no triangle emits, or the probe's line passes no emitter's
+                            // leaf box: the probe's emitter pass ends with no hit, exactly
+                            // as a traversal would (the ray is still counted: the
+                            // reference traces it)
                             ++c_trav;
                             ++c_local;
                             put_level(kNoProbe, direct);
                             after = true;
-                        } else if (INL) {
+                        } else if (INL && TPT_PROBE_INLINE) {
+                            tg = grazing(gpass, td);
                             // <= 4 emitters: pass 1 here; a miss resolves the probe in
                             // this pass, an emitter hit goes on to pass 2 (occlusion)
                             ++c_trav;
@@ -1285,6 +1336,7 @@ void k_trace(TraceArgs a) {
                                 }
                             }
                         } else {
+                            tg = grazing(gpass, td);
                             phase = PH_PROBE;
                         }
                     } else {
@@ -1733,6 +1785,7 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
                                 : no_surface();
             trav_begin(r, ro, rdir, tm, a.boxes_finite != 0, a.emit_root, a.cull_eps, grazing(gs, rdir));
             uint32_t c_leaf = 0;
+            if (mode == 3 && probe_misses_emitters(a, ro, rdir)) r.node = -1;   // the render's probe pre-test
             trav_lane<true>(r, a, stk, c_ovf);
             if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
             if (mode == 3 && r.mode == TM_EMIT && r.fid >= 0) {   // pass 2: does anything beat the emitter hit?
@@ -1830,7 +1883,7 @@ static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s)
 // pair mode (delta-light scenes only).
 template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false, bool ENVIS = false, bool DRAIN = false>
 static void launch_ordered_d(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    if (a.emit_inline) {
+    if (TPT_PROBE_INLINE && a.emit_inline) {
         if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR, DRAIN>(a, grid, lds, s);
         else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR, DRAIN>(a, grid, lds, s);
     } else {
