@@ -639,10 +639,29 @@ __device__ __forceinline__ void sliver_pass(Trav& r, const TraceArgs& a, uint32_
 
 __device__ __forceinline__ V3 reflect_dir(V3 d, V3 n) { return d - (2.0f * dot(d, n)) * n; }   // :137-141
 
+// HemisphereCosine's frame (sampler.h:75-89) for the incident-side normal:
+// getNewDirection flips n toward the incident side (path_tracer.cu:216-218),
+// then xBase = (1, 0, -n.x / n.z) / |.| (or (0, 0, 1)), zBase = xBase x n.
+// The direct probe (:387-389) samples the same hemisphere as the bounce's
+// extension ray (same incident direction and normal), so a shading pass
+// computes the frame once and both samples use it (the same values as two
+// evaluations: bit-identical).
+struct Hemi {
+    V3 n, xb;
+};
+__device__ __forceinline__ Hemi hemi_basis(V3 d, V3 n) {
+    const float sign = dot(d, n) > 0.0f ? -1.0f : 1.0f;
+    n = sign * n;
+    V3 xb = n.z == 0.0f ? v3(0.0f, 0.0f, 1.0f) : v3(1.0f, 0.0f, -n.x / n.z);
+    xb = vdiv(xb, fsqrt(norm2(xb)));
+    return Hemi{n, xb};
+}
+
 // getNewDirection (path_tracer.cu:187-225) for a material (eta, metallic).
 // Returns the pdf; consumes 1 (dielectric), 0 (metal) or 2 (diffuse) uniforms.
+// hb / hb_ok: the pass's hemisphere frame for (d, n), computed on first use.
 __device__ __forceinline__ float new_direction(V3 d, V3 n, float eta_m, float metallic, uint32_t st[6], V3& next,
-                                               float& atten) {
+                                               float& atten, Hemi& hb, bool& hb_ok) {
     if (eta_m > 0.0f) {
         // refract (:143-163)
         float cos_i = dot(d, n);
@@ -672,11 +691,13 @@ __device__ __forceinline__ float new_direction(V3 d, V3 n, float eta_m, float me
         next = reflect_dir(d, n);
         return 1.0f;
     }
-    const float sign = dot(d, n) > 0.0f ? -1.0f : 1.0f;
-    n = sign * n;
+    if (!hb_ok) {
+        hb = hemi_basis(d, n);
+        hb_ok = true;
+    }
+    n = hb.n;
+    const V3 xb = hb.xb;
     // HemisphereCosine (sampler.h:75-89)
-    V3 xb = n.z == 0.0f ? v3(0.0f, 0.0f, 1.0f) : v3(1.0f, 0.0f, -n.x / n.z);
-    xb = vdiv(xb, fsqrt(norm2(xb)));
     const V3 zb = cross(xb, n);
     const float phi = 2.0f * kPi * xorwow_uniform(st);
     const float cos_t = fsqrt(xorwow_uniform(st));
@@ -1183,6 +1204,8 @@ void k_trace(TraceArgs a) {
             TPT_SEC_BEGIN()
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
             bool finish = false, lights_next = false, after = false;
+            Hemi hb;              // this pass's hemisphere frame (new_direction), shared by the
+            bool hb_ok = false;   // bounce's extension sample and its direct probe
             bool begun = false;   // the next ray is already set up (inline probe pass 1)
             V3 L = v3(0.0f, 0.0f, 0.0f);
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
@@ -1204,7 +1227,7 @@ void k_trace(TraceArgs a) {
                     const int mtl = __float_as_int(s0.w);
                     const float4 m1 = MT(2 * mtl + 1);
                     float af;
-                    const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af);
+                    const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af, hb, hb_ok);
                     graze_next = grazing(gpass, nd);
                     rec.put(depth, 0, af);
                     mk = (uint32_t)mtl | (p_kind(prob) << 30);
@@ -1301,7 +1324,7 @@ void k_trace(TraceArgs a) {
                         ts = TS_IDLE;
                     } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
                         float af2;
-                        new_direction(rd, nrm, m1.x, m1.y, st, td, af2);
+                        new_direction(rd, nrm, m1.x, m1.y, st, td, af2, hb, hb_ok);
                         if ((TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) ||
                             (ORDERED && probe_misses_emitters(a, r.o, td))) {
                             // no triangle emits, or the probe's line passes no emitter's
