@@ -79,6 +79,9 @@
 // shading pass and the others trace pass 1 as a traversal.
 #define TPT_PROBE_INLINE 0
 #endif
+#ifndef TPT_SHARE_HEMI
+#define TPT_SHARE_HEMI 0   // 1: the direct probe reuses the extension sample's hemisphere frame (new_direction)
+#endif
 #ifndef TPT_ENV_INLINE
 #define TPT_ENV_INLINE 0   // 1: env_lookup inlined in every variant (A/B builds)
 #endif
@@ -1324,6 +1327,7 @@ void k_trace(TraceArgs a) {
                         ts = TS_IDLE;
                     } else if (!(m1.x >= 1.0f || m1.y > 0.0f)) {   // direct probe (:387-389)
                         float af2;
+                        if (!TPT_SHARE_HEMI) hb_ok = false;   // (A/B builds: the frame recomputed)
                         new_direction(rd, nrm, m1.x, m1.y, st, td, af2, hb, hb_ok);
                         if ((TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) ||
                             (ORDERED && probe_misses_emitters(a, r.o, td))) {

@@ -123,7 +123,7 @@ def main():
         return sec
 
     cur_file, cur_line, last_main = None, 0, 0
-    caller = "kernel prologue"   # the last non-traversal section seen (the caller of shared helpers)
+    cur_sec = ["kernel prologue"]
     inside = False
     depth = 0
     for line in open(asm):
@@ -140,24 +140,31 @@ def main():
         if s.startswith(".loc"):
             p = s.split()
             cur_file, cur_line = files.get(p[1], p[1]), int(p[2])
-            if cur_file and cur_file.endswith(srcname) and cur_line > 0:
-                last_main = cur_line
-                sec = section_of(cur_line)
-                if not sec.startswith("trav") and sec != "helper":
-                    caller = sec
+            # the comment holds the inlining chain: loc @[ caller @[ caller's caller ] ]
+            chain = re.findall(r"([\w./-]+):(\d+)(?::\d+)?", line.split(";", 1)[1]) if ";" in line else []
+            main = [int(l) for f, l in chain if f.endswith(srcname) and int(l) > 0]
+            if main:
+                # the outermost function below k_trace that owns a section decides
+                # (slab_minmax inside probe_misses_emitters is the probe pre-test);
+                # otherwise the k_trace call-site line does
+                site = main[-1]
+                named = [section_of(l) for l in main[:-1]]
+                named = [x for x in named if x not in ("helper", "other") and not x.startswith(("kernel", "pass: consume",
+                         "pass: lights", "pass: after", "pass: unwind", "pass: camera", "pass: exit", "pass: sliver /"))]
+                sec = named[-1] if named else section_of(site)
+                if sec == "helper":
+                    sec = section_of(site)
+                last_main = site
+                cur_sec[0] = sec
             continue
         if not s or s.startswith((".", ";")) or s.endswith(":"):
             continue
         c = classify(s.split()[0])
         if c is None:
             continue
-        sec = section_of(last_main)
-        # box / slab / triangle helpers outside the traversal loop (depth >= 2)
-        # belong to their caller in the shading pass (sliver re-test, probe pre-test)
-        if (sec.startswith("trav") and depth < 2) or (sec == "helper" and depth < 2):
-            sec = caller
-        elif sec == "helper":
-            sec = "trav: loop control, stack pop, leaf park"
+        sec = cur_sec[0]
+        if sec == "helper" or (sec.startswith("trav") and depth < 2):
+            sec = "other"
         counts[sec][c] += 1
     cols = ["valu", "salu", "vmem", "smem", "lds", "scratch", "branch", "wait"]
     order = sorted(counts, key=lambda k: (not k.startswith("trav"), k))
