@@ -252,3 +252,49 @@ def test_logged_baseline_divergences_are_fixed(scenes):
         h1, t1, uv1 = d.trace_rays(o, di, mode=1)
         assert np.array_equal(h1, h0) and np.array_equal(_bits(t1), _bits(t0)) and np.array_equal(_bits(uv1), _bits(uv0))
         _check_modes(s, d, o, di, h0, t0, uv0)
+
+
+@pytest.mark.parametrize("name", ["box", "box2", "tir", "c5"])
+def test_probe_pretest_exact_near_emitter_boxes(scenes, name):
+    """The direct probe's pre-test (trace.hip probe_misses_emitters: a slab test
+    of the emitters' enclosing boxes with approximate reciprocals and a margin)
+    must never call a probe a miss when the reference's closest hit is an
+    emitter.  Rays aimed at the emissive triangles' vertices, edges and leaf-box
+    corners, nudged by 0..4 ulps and by 1e-7..1e-3 relative, from origins all
+    over the scene (and a quarter skimming the emitter's plane): mode 3 equals
+    "the reference-order closest hit is an emitter" on every ray."""
+    s, d = scenes[name]
+    emit = _emissive_faces(s)
+    wv, _ = d.read_world()
+    tri = s.indices.reshape(-1, 3)[emit]
+    assert len(tri) > 0
+    rng = np.random.default_rng(7 + len(tri))
+    n = 400_000
+    k = rng.integers(0, len(tri), n)
+    v = wv[tri[k]].astype(np.float32)                                 # (n, 3 verts, 3)
+    lo, hi = v.min(1), v.max(1)
+    w = rng.uniform(0, 1, (n, 1)).astype(np.float32)
+    a, b = rng.integers(0, 3, n), rng.integers(0, 3, n)
+    edge = (v[np.arange(n), a] + w * (v[np.arange(n), b] - v[np.arange(n), a])).astype(np.float32)
+    corner = np.where(rng.uniform(size=(n, 3)) < 0.5, lo, hi).astype(np.float32)
+    sel = rng.integers(0, 3, (n, 1))
+    tgt = np.where(sel == 0, v[np.arange(n), a], np.where(sel == 1, edge, corner)).astype(np.float32)
+    rel = (10.0 ** rng.uniform(-7, -3, (n, 1)) * rng.choice([-1.0, 0.0, 1.0], (n, 3))).astype(np.float32)
+    tgt = (tgt * (1 + rel)).astype(np.float32)
+    ul = rng.integers(-4, 5, (n, 3)).astype(np.int32)
+    tgt = (tgt.view(np.int32) + ul).view(np.float32)
+    glo, ghi = wv.min(0), wv.max(0)
+    org = (glo + (ghi - glo) * rng.uniform(-0.1, 1.1, (n, 3))).astype(np.float32)
+    # a quarter start in the emitter's own plane region (skimming rays)
+    skim = rng.uniform(size=n) < 0.25
+    org[skim] = (tgt[skim] + (tgt[skim] - org[skim]) * np.float32(-0.5)).astype(np.float32)
+    org[skim, 1] = tgt[skim, 1]
+    dirs = (tgt - org).astype(np.float32)
+    ok = np.isfinite(dirs).all(1) & (np.abs(dirs).sum(1) > 0)
+    org, dirs = org[ok], dirs[ok]
+    h0, t0, uv0 = d.trace_rays(org, dirs, mode=0)
+    emit_hit = (h0 >= 0) & emit[np.maximum(h0, 0)]
+    assert emit_hit.mean() > 0.05, emit_hit.mean()
+    h3, _, _ = d.trace_rays(org, dirs, mode=3)
+    assert np.array_equal(h3 >= 0, emit_hit), int(((h3 >= 0) != emit_hit).sum())
+    assert np.array_equal(h3[emit_hit], h0[emit_hit])

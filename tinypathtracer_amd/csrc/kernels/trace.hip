@@ -1146,6 +1146,10 @@ void k_trace(TraceArgs a) {
 #ifdef TPT_PROFILE_PHASES
     const unsigned long long t_wave0 = wall_clock64();
     unsigned long long p_done = 0, p_trav = 0, p_steps = 0, t_iter0 = 0, t_loop0 = 0, p_outer = 0;
+    // lane states summed over traversal steps (DESIGN.md "N1"): traversing, a
+    // finished ray waiting for the wave's next shading pass, no work (pixel done
+    // or none, pair-mode idle); and the lanes each shading pass serves
+    unsigned long long p_lt = 0, p_lw = 0, p_lx = 0, p_lp = 0;
     // shading-pass sections (profiling builds only): every boundary drains
     // the wave's outstanding memory operations, so a section is charged the
     // latency of its own loads; the pass's first active lane adds the time
@@ -1202,6 +1206,9 @@ void k_trace(TraceArgs a) {
             vpend = false;
             verify_ray(a, r, phase, a.mtl);
         }
+#endif
+#ifdef TPT_PROFILE_PHASES
+        if (__ballot(ts == TS_DONE) != 0ull) p_lp += (unsigned long long)__popcll(__ballot(ts == TS_DONE));
 #endif
         if (ts == TS_DONE) {
             TPT_SEC_BEGIN()
@@ -1593,6 +1600,11 @@ void k_trace(TraceArgs a) {
             ++p_steps;
 #endif
             const int cnt = __popcll(__ballot(ts == TS_TRAV));
+#ifdef TPT_PROFILE_PHASES
+            p_lt += (unsigned long long)cnt;
+            p_lw += (unsigned long long)__popcll(__ballot(ts == TS_DONE));
+            p_lx += (unsigned long long)__popcll(__ballot(ts == TS_DEAD || ts == TS_IDLE));
+#endif
             if (cnt == 0) break;
             if (cnt < thr && __ballot(ts == TS_DONE) != 0ull) break;
             // Speculative leaf postponement: a lane that reaches a leaf parks it
@@ -1698,6 +1710,10 @@ void k_trace(TraceArgs a) {
         atomicAdd(&a.counters[7], p_trav);
         atomicAdd(&a.counters[8], p_steps);
         atomicAdd(&a.counters[12], p_outer);
+        atomicAdd(&a.counters[25], p_lt);
+        atomicAdd(&a.counters[26], p_lw);
+        atomicAdd(&a.counters[27], p_lx);
+        atomicAdd(&a.counters[28], p_lp);
         const unsigned long long life = wall_clock64() - t_wave0;
         atomicMax(&a.counters[13], life);
         atomicAdd(&a.counters[14], life);

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Lane states of the trace kernel (DESIGN.md "N1: cross-wave compaction"): the
+# phase-profiling build (variants/prof, -DTPT_PROFILE_PHASES) counts, per
+# traversal step, the lanes traversing / holding a finished ray that waits for
+# the wave's next shading pass / without work, and the lanes each shading pass
+# serves.  One 256-spp full-frame launch per config.
+# Usage: bash tools/gpu_lanes.sh "C2 C5" [extra bench args]
+set -o pipefail
+export TMPDIR=/tmp
+CFGS=${1:-"C2 C5"}; shift; EXTRA="$@"
+mkdir -p gpurun_out
+for C in $CFGS; do
+  TPT_LIB=$PWD/tinypathtracer_amd/variants/prof/libtpt.so TPT_DEBUG_COUNTERS=1 \
+    timeout -k 10 300 python bench.py --config $C --spp 256 --pipe-sets 1 --steps 1 --warmup 0 --cpu-baseline 0 $EXTRA \
+    > gpurun_out/lanes_$C.json 2> gpurun_out/lanes_$C.err || { tail -5 gpurun_out/lanes_$C.err; exit 1; }
+  python3 - "$C" gpurun_out/lanes_$C.err <<'PY'
+import sys
+c = [int(x) for x in [l for l in open(sys.argv[2]) if l.startswith("tpt counters")][-1].split(":")[1].split()]
+steps, passes, lt, lw, lx, lp = c[8], c[12], c[25], c[26], c[27], c[28]
+tot = lt + lw + lx
+print(f"{sys.argv[1]}: steps {steps} passes {passes} steps/pass {steps / max(passes, 1):.2f} | lane-steps: traversing "
+      f"{lt / tot:.3f} waiting-for-pass {lw / tot:.3f} no-work {lx / tot:.3f} | lanes per pass {lp / max(passes, 1):.1f} | "
+      f"shading ticks {c[6]} traversal ticks {c[7]}")
+PY
+done
