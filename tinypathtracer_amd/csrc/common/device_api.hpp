@@ -106,6 +106,9 @@ struct TraceArgs {
     int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
     int32_t drained;                     // 1: the launch cannot fill the chip (latency-oriented DRAIN variants)
     int32_t xcd_run;                     // > 0: workgroup tiles dealt to XCDs in runs of this many (k_trace)
+    int32_t tile_pool;                   // 1: each workgroup renders two adjacent tiles, the second as a pixel
+                                         //    pool its finished lanes draw from (k_trace; set by launch_trace)
+    int32_t lds_pool_offset;             // set by launch_trace: byte offset of the pool counter in LDS
     int32_t lds_rec_offset;              // set by launch_trace: byte offset of the record region
     int32_t rec_lds_levels;              // set by launch_trace: path-record levels held in LDS
     int32_t stack_lds_slots;             // set by launch_trace: stack slots held in LDS (rest private)

@@ -69,6 +69,12 @@
 // DRAIN variants (launches that cannot fill the chip: a few waves per SIMD anyway)
 #define TPT_TRACE_WAVES_DRAIN 4
 #endif
+#ifndef TPT_TILE_POOL
+// 1: one-lane-per-pixel, full-occupancy launches give each workgroup two
+// adjacent 16x16 tiles; the second is a pixel pool its finished lanes draw
+// from ("Round 4: N1").  0: one tile per workgroup.
+#define TPT_TILE_POOL 1
+#endif
 #ifndef TPT_ENV_FAST
 #define TPT_ENV_FAST 1     // env texel indices from fp32 bounds, double trig only near texel edges (0: A/B builds)
 #endif
@@ -1025,18 +1031,27 @@ void k_trace(TraceArgs a) {
         bx = ((m / g) * 8 + k) * g + m % g;
     }
     const int frame = by % nfr;
+    // Pixel pool (round 4; DESIGN.md section 5 "Round 4: N1"): workgroup b renders
+    // tiles 2b and 2b + 1 of its row.  Its lanes start on the first; a lane whose
+    // pixel has run all its samples stores it and takes the next unclaimed pixel
+    // of the second (an LDS counter), so the lanes of cheap pixels (misses, walls)
+    // keep working while their wave's heavy pixels finish.  Every pixel still runs
+    // all its samples in order on one lane with its own XORWOW stream: the image
+    // is bit-identical to one tile per workgroup.
+    const bool pool = !PAIR && !DRAIN && TPT_TILE_POOL && a.tile_pool > 0;
+    const int tx = pool ? 2 * bx : bx;
     // pair mode: lane 2q (path) and 2q + 1 (side) serve pixel q of the wave's 8x4 tile
     const bool side = PAIR && (lane & 1);
     const int pl = PAIR ? (lane >> 1) : lane;   // pixel slot in the wave
-    const int x = bx * 16 + (wave & 1) * 8 + (pl & 7);
+    int x = tx * 16 + (wave & 1) * 8 + (pl & 7);
     const int ly = PAIR ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3) : (by / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
-    const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
+    int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
     const bool pixel = x < a.width && ly < a.band_height && y < a.height;
-    const bool active = pixel && !side;   // owns the pixel's RNG stream and sums
+    bool active = pixel && !side;   // owns the pixel's RNG stream and sums
     uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
     uint32_t c_local = 0;   // rays resolved in the shading pass without a BVH traversal
     const size_t npix = (size_t)a.width * (size_t)a.height;
-    const size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
+    size_t off = active ? (size_t)x + (size_t)y * (size_t)a.width : 0;
     // frame batch: each frame owns its own RNG and accumulator planes
     uint32_t* const g_rng = a.rng + (size_t)frame * 6 * npix;
     float* const g_acc = a.accum + (size_t)frame * 3 * npix;
@@ -1065,7 +1080,9 @@ void k_trace(TraceArgs a) {
         snodes[i].z = m.z;
         snodes[i].w = m.w;
     }
-    if (MTL_LDS || a.lds_nodes > 0) __syncthreads();
+    TPT_LDS int* pool_next = (TPT_LDS int*)(slds + a.lds_pool_offset);   // next unclaimed pixel of tile 2b + 1
+    if (pool && tid == 0) *pool_next = 0;
+    if (MTL_LDS || a.lds_nodes > 0 || pool) __syncthreads();
     auto MT = [&](int i) -> float4 {
         if constexpr (MTL_LDS) {
             return make_float4(smtl[i].x, smtl[i].y, smtl[i].z, smtl[i].w);
@@ -1474,6 +1491,34 @@ void k_trace(TraceArgs a) {
             }
             TPT_SEC(4)
             V3 to = r.o;
+            if (pool && phase == PH_CAMERA && remaining == 0 && active) {
+                // this pixel is done: store it and draw the next pixel of the pool tile
+#pragma unroll
+                for (int i = 0; i < 6; ++i) g_rng[i * npix + off] = st[i];
+                g_acc[off] = total.x;
+                g_acc[npix + off] = total.y;
+                g_acc[2 * npix + off] = total.z;
+                active = false;
+                for (;;) {
+                    const int j = __atomic_fetch_add(pool_next, 1, __ATOMIC_RELAXED);
+                    if (j >= 256) break;
+                    const int wj = j >> 6, lj = j & 63;
+                    const int px = (tx + 1) * 16 + (wj & 1) * 8 + (lj & 7);
+                    const int ply = (by / nfr) * 16 + (wj >> 1) * 8 + (lj >> 3);
+                    const int py = band_row(ply, a.band_rows, a.band_count, a.band_index);
+                    if (px < a.width && ply < a.band_height && py < a.height) {
+                        x = px;
+                        y = py;
+                        off = (size_t)x + (size_t)y * (size_t)a.width;
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) st[i] = g_rng[i * npix + off];
+                        total = v3(g_acc[off], g_acc[npix + off], g_acc[2 * npix + off]);
+                        remaining = a.samples;
+                        active = true;
+                        break;
+                    }
+                }
+            }
             if (phase == PH_CAMERA) {
                 if (remaining == 0) {
                     ts = TS_DEAD;
@@ -2002,6 +2047,8 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
+    a.tile_pool = 0;
+    a.lds_pool_offset = 0;
     dim3 grid((a.width + 15) / 16, ((a.band_height + 15) / 16) * (a.n_frames > 0 ? a.n_frames : 1));
     // the XCD-run remap is a permutation of a row's tiles only if runs tile gridDim.x / 8
     if (a.xcd_run > 0 && (grid.x % 8 != 0 || (grid.x / 8) % (unsigned)a.xcd_run != 0)) a.xcd_run = 0;
@@ -2051,7 +2098,17 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    const size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true);
+    // pixel pool (k_trace): two tiles per workgroup, the second drawn from by the
+    // lanes that finish their pixel first; its LDS counter comes out of the budget
+    const bool use_pool = TPT_TILE_POOL && !a.drained;
+    size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudget - (use_pool ? 16 : 0));
+    if (use_pool) {
+        a.tile_pool = 1;
+        grid.x = (grid.x + 1) / 2;
+        if (a.xcd_run > 0 && (grid.x % 8 != 0 || (grid.x / 8) % (unsigned)a.xcd_run != 0)) a.xcd_run = 0;
+        a.lds_pool_offset = (int)((lds + 15) / 16 * 16);
+        lds = (size_t)a.lds_pool_offset + 16;
+    }
     if (lights) {
         if (mtl_lds) {
             if (small) launch_ordered<true, true, uint16_t>(a, grid, lds, s);
