@@ -144,7 +144,9 @@ CASES = [
     ("light", 64, 36, 8, 8, "sky"),
     ("box1", 40, 24, 8, 8, "sky"),
     ("c5", 96, 54, 8, 8, None),   # 131,712 triangles: 32-bit stack ids, LDS + private stack
-    ("c5", 256, 40, 2, 8, None),  # 16 tiles per row: XCD runs of 2 (k_trace prologue)
+    ("c5", 512, 24, 2, 8, None),  # 32 tiles per row, 16 two-tile workgroups: XCD runs of 2 (k_trace prologue)
+    ("box", 72, 40, 8, 8, None),  # 5 tiles per row: the last workgroup's pixel pool is empty
+    ("tir", 88, 20, 8, 16, None),  # 6 tiles, the last one partial (x 80..87): pool pixels skipped
 ]
 
 

@@ -1081,7 +1081,7 @@ void k_trace(TraceArgs a) {
         snodes[i].w = m.w;
     }
     TPT_LDS int* pool_next = (TPT_LDS int*)(slds + a.lds_pool_offset);   // next unclaimed pixel of tile 2b + 1
-    if (pool && tid == 0) *pool_next = 0;
+    if (pool && tid == 0) *pool_next = (tx + 1) * 16 < a.width ? 0 : 256;   // (no second tile: an empty pool)
     if (MTL_LDS || a.lds_nodes > 0 || pool) __syncthreads();
     auto MT = [&](int i) -> float4 {
         if constexpr (MTL_LDS) {
@@ -2105,7 +2105,12 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     if (use_pool) {
         a.tile_pool = 1;
         grid.x = (grid.x + 1) / 2;
-        if (a.xcd_run > 0 && (grid.x % 8 != 0 || (grid.x / 8) % (unsigned)a.xcd_run != 0)) a.xcd_run = 0;
+        if (a.xcd_run > 0) {   // runs of workgroups now: half as many, each two tiles wide
+            const int per = grid.x % 8 == 0 ? (int)grid.x / 8 : 0, want = std::max(2, a.xcd_run / 2);
+            a.xcd_run = 0;
+            for (int g = std::min(per, want); g >= 2 && a.xcd_run == 0; --g)
+                if (per % g == 0) a.xcd_run = g;
+        }
         a.lds_pool_offset = (int)((lds + 15) / 16 * 16);
         lds = (size_t)a.lds_pool_offset + 16;
     }
