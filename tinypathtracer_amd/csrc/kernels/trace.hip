@@ -72,8 +72,11 @@
 #ifndef TPT_TILE_POOL
 // 1: one-lane-per-pixel, full-occupancy launches give each workgroup two
 // adjacent 16x16 tiles; the second is a pixel pool its finished lanes draw
-// from ("Round 4: N1").  0: one tile per workgroup.
-#define TPT_TILE_POOL 1
+// from ("Round 4: N1").  0 (default): one tile per
+// workgroup -- the pool measured C2 -15 %, C4 -39 %, C5 -5 % (workgroups live
+// twice as long, so a launch's tail of heavy workgroups grows, while lanes
+// without work were only 7.6 % of C2's lane-steps).
+#define TPT_TILE_POOL 0
 #endif
 #ifndef TPT_ENV_FAST
 #define TPT_ENV_FAST 1     // env texel indices from fp32 bounds, double trig only near texel edges (0: A/B builds)
