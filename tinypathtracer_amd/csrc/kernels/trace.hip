@@ -179,8 +179,15 @@ __device__ __forceinline__ bool box_hit(const V3& o, const V3& inv, float nx, fl
 //     28 %: boxes just behind a secondary ray's origin are entered again.);
 //   * rays grazing a triangle's plane (|cos| < ~1e-4) have the same
 //     ill-conditioned t; origins exactly on an edge or vertex with such
-//     directions diverge at ~1e-3 of adversarial rays (tests/test_gpu_cull.py)
-//     and none of the BASELINE frames' rays (tests/test_gpu_fullsize.py).
+//     directions diverge at ~1e-3 of adversarial rays (tests/test_gpu_cull.py):
+//     a ray leaving a face within 1e-3 of its plane takes the uncull'd binary
+//     path from the start;
+//   * grazing hits (round 4): a ray that meets a shared edge at a grazing
+//     angle to both faces gets a neighbour's t a long way outside that
+//     neighbour's box (C5 at 2048 spp: 2 rays of 105 G, |cos| 4e-5 and 1e-4,
+//     t 1.5e-4 and 3.9e-4 relative before the box); a closest hit (or probe
+//     emitter hit) found by the culled walk on a face met within 1e-3 of its
+//     plane sends the ray again through the uncull'd binary path.
 //  Modes:
 //   TM_CLOSEST  closest hit (extension and camera rays; probes in reference order)
 //   TM_ANY      shadow rays stop at the first accepted triangle (only
@@ -658,15 +665,28 @@ __device__ __forceinline__ V3 reflect_dir(V3 d, V3 n) { return d - (2.0f * dot(d
 // extension ray (same incident direction and normal), so a shading pass
 // computes the frame once and both samples use it (the same values as two
 // evaluations: bit-identical).
+// TPT_SHARE_HEMI 1 keeps the whole frame (6 floats) for the probe; 2 keeps
+// only the two values that cost divides and a sqrt -- q = -n.x / n.z and
+// r = 1 / |xBase| -- and rebuilds n, xBase = r * (1, 0, q) (or r * (0, 0, 1))
+// from them: the same values, two live registers instead of six.
 struct Hemi {
     V3 n, xb;
+    float q, r;
 };
 __device__ __forceinline__ Hemi hemi_basis(V3 d, V3 n) {
     const float sign = dot(d, n) > 0.0f ? -1.0f : 1.0f;
     n = sign * n;
-    V3 xb = n.z == 0.0f ? v3(0.0f, 0.0f, 1.0f) : v3(1.0f, 0.0f, -n.x / n.z);
-    xb = vdiv(xb, fsqrt(norm2(xb)));
-    return Hemi{n, xb};
+    const float q = n.z == 0.0f ? 0.0f : -n.x / n.z;
+    V3 xb = n.z == 0.0f ? v3(0.0f, 0.0f, 1.0f) : v3(1.0f, 0.0f, q);
+    const float r = 1.0f / fsqrt(norm2(xb));   // vdiv(xb, s) == (1 / s) * xb
+    xb = r * xb;
+    return Hemi{n, xb, q, r};
+}
+__device__ __forceinline__ Hemi hemi_rebuild(V3 d, V3 n, float q, float r) {
+    const float sign = dot(d, n) > 0.0f ? -1.0f : 1.0f;
+    n = sign * n;
+    const V3 xb = r * (n.z == 0.0f ? v3(0.0f, 0.0f, 1.0f) : v3(1.0f, 0.0f, q));
+    return Hemi{n, xb, q, r};
 }
 
 // getNewDirection (path_tracer.cu:187-225) for a material (eta, metallic).
@@ -703,7 +723,9 @@ __device__ __forceinline__ float new_direction(V3 d, V3 n, float eta_m, float me
         next = reflect_dir(d, n);
         return 1.0f;
     }
-    if (!hb_ok) {
+    if (TPT_SHARE_HEMI == 2 && hb_ok) {
+        hb = hemi_rebuild(d, n, hb.q, hb.r);
+    } else if (!hb_ok) {
         hb = hemi_basis(d, n);
         hb_ok = true;
     }
@@ -924,7 +946,7 @@ __device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int p
     o[12] = (unsigned long long)(long long)r.hpos;
     o[13] = (unsigned long long)(long long)q.hpos;
     o[14] = __float_as_uint(r.u);
-    o[15] = __float_as_uint(q.u);
+    o[15] = (unsigned long long)(r.fin ? 1u : 0u) | ((unsigned long long)__float_as_uint(r.lim) << 32);   // culled path?, final entry-cull bound
 }
 #endif
 // TS_IDLE (pair mode): a side lane without a job, or a path lane waiting for
@@ -1211,6 +1233,14 @@ void k_trace(TraceArgs a) {
             }
         }
 #endif
+        if (ORDERED && ts == TS_DONE && r.fin && r.fid >= 0 && (r.mode == TM_CLOSEST || r.mode == TM_EMIT) && a.graze &&
+            grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
+            // a grazing hit (Culling: "Grazing hits"): the same ray again on the
+            // uncull'd binary path, which tests every leaf whose box its line passes
+            trav_begin(r, r.o, r.d, r.mode, a.boxes_finite != 0, a.emit_root, a.cull_eps, true);
+            ts = TS_TRAV;
+            sl_pend = false;
+        }
         if (ORDERED && ts == TS_DONE && phase == PH_PROBE && r.mode == TM_EMIT && r.fid >= 0) {
             // direct probe, pass 2: the emitter hit stands unless something
             // beats it -- restart from the root keeping its t, position and fid
@@ -1879,6 +1909,12 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
             if (mode == 3 && probe_misses_emitters(a, ro, rdir)) r.node = -1;   // the render's probe pre-test
             trav_lane<true>(r, a, stk, c_ovf);
             if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
+            if (r.fin && r.fid >= 0 && (r.mode == TM_CLOSEST || r.mode == TM_EMIT) && a.graze &&
+                grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
+                // the render's grazing-hit rule: traced again on the uncull'd binary path
+                trav_begin(r, ro, rdir, r.mode, a.boxes_finite != 0, a.emit_root, a.cull_eps, true);
+                trav_lane<true>(r, a, stk, c_ovf);
+            }
             if (mode == 3 && r.mode == TM_EMIT && r.fid >= 0) {   // pass 2: does anything beat the emitter hit?
                 r.mode = TM_OCCL;
                 r.node = 0;

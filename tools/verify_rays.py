@@ -27,5 +27,10 @@ for spec in sys.argv[1:]:
     for mode in (0, 1, 2):
         h, t, uv = ds.trace_rays(o, di, mode=mode)
         print(cfg, "mode", mode, "hit", h.tolist(), "t", [f"{x:.9g}" for x in t])
-    print(cfg, "logged render: culled fid", d[:, 2].astype(np.int64).tolist(), "ref fid", d[:, 3].astype(np.int64).tolist())
+    print(cfg, "logged render: culled fid", d[:, 2].astype(np.int64).tolist(), "ref fid", d[:, 3].astype(np.int64).tolist(),
+          "mode", d[:, 0].tolist(), "phase", d[:, 1].tolist(), "culled path", (d[:, 15] & 1).tolist(),
+          "t culled", [f"{x:.9g}" for x in f32(d[:, 4])], "t ref", [f"{x:.9g}" for x in f32(d[:, 5])],
+          "lim", [f"{x:.9g}" for x in f32(d[:, 15] >> 32)], "hpos", d[:, 12].astype(np.int64).tolist(),
+          "ref hpos", d[:, 13].astype(np.int64).tolist())
+    print(cfg, "o", o.tolist(), "d", di.tolist())
     ds.close()
