@@ -69,6 +69,9 @@
 // DRAIN variants (launches that cannot fill the chip: a few waves per SIMD anyway)
 #define TPT_TRACE_WAVES_DRAIN 4
 #endif
+#ifndef TPT_GRAZE_HIT   // the grazing-hit rule (Culling: "Grazing hits"); 0 only to measure its cost
+#define TPT_GRAZE_HIT 1
+#endif
 #ifndef TPT_TILE_POOL
 // 1: one-lane-per-pixel, full-occupancy launches give each workgroup two
 // adjacent 16x16 tiles; the second is a pixel pool its finished lanes draw
@@ -1233,10 +1236,11 @@ void k_trace(TraceArgs a) {
             }
         }
 #endif
-        if (ORDERED && ts == TS_DONE && r.fin && r.fid >= 0 && (r.mode == TM_CLOSEST || r.mode == TM_EMIT) && a.graze &&
-            grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
-            // a grazing hit (Culling: "Grazing hits"): the same ray again on the
+        if (TPT_GRAZE_HIT && ORDERED && ts == TS_DONE && phase == PH_PROBE && r.fin && r.fid >= 0 && r.mode == TM_EMIT &&
+            a.graze && grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
+            // a grazing probe hit (Culling: "Grazing hits"): pass 1 again on the
             // uncull'd binary path, which tests every leaf whose box its line passes
+            // (an extension ray's grazing hit is caught in its shading prelude)
             trav_begin(r, r.o, r.d, r.mode, a.boxes_finite != 0, a.emit_root, a.cull_eps, true);
             ts = TS_TRAV;
             sl_pend = false;
@@ -1270,32 +1274,39 @@ void k_trace(TraceArgs a) {
             V3 L = v3(0.0f, 0.0f, 0.0f);
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
             Surf gpass = gsurf;   // the face this pass's new rays leave
+            bool redo = false;    // a grazing extension hit: traced again, uncull'd
             if (phase == PH_EXT) {
                 if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
                     if (a.env) L = env_lookup<ENVIS>(a.env, a.env_w, a.env_h, rd);
                     finish = true;
                 } else {           // hit shading prelude (:364-381)
-                    ++c_shade;
                     const float4* sh = a.shade + 3 * r.fid;
                     const float4 s0 = sh[0], s1 = sh[1], s2 = sh[2];
-                    const float w = 1.0f - r.u - r.v;
-                    nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (r.u * v3(s1.x, s1.y, s1.z))) +
-                                    (r.v * v3(s2.x, s2.y, s2.z)));
-                    gpass = a.graze ? Surf{s1.w, s2.w} : no_surface();
-                    if constexpr (LIGHTS) gsurf = gpass;
-                    r.o = r.o + (r.t * rd);
-                    const int mtl = __float_as_int(s0.w);
-                    const float4 m1 = MT(2 * mtl + 1);
-                    float af;
-                    const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af, hb, hb_ok);
-                    graze_next = grazing(gpass, nd);
-                    rec.put(depth, 0, af);
-                    mk = (uint32_t)mtl | (p_kind(prob) << 30);
-                    direct = v3(0.0f, 0.0f, 0.0f);
-                    li = 0;
-                    delegated = false;
-                    env_pending = ENVIS && !(m1.x > 0.0f) && !(m1.y > 0.0f);   // diffuse hit
-                    lights_next = true;
+                    // the grazing-hit rule (Culling: "Grazing hits"): a culled walk's hit
+                    // within 1e-3 of the face's plane is not shaded; the same ray is traced
+                    // again on the uncull'd binary path (ray set-up below, not counted)
+                    redo = TPT_GRAZE_HIT && ORDERED && r.fin && a.graze && grazing(Surf{s1.w, s2.w}, rd);
+                    if (!redo) {
+                        ++c_shade;
+                        const float w = 1.0f - r.u - r.v;
+                        nrm = normalize(((w * v3(s0.x, s0.y, s0.z)) + (r.u * v3(s1.x, s1.y, s1.z))) +
+                                        (r.v * v3(s2.x, s2.y, s2.z)));
+                        gpass = a.graze ? Surf{s1.w, s2.w} : no_surface();
+                        if constexpr (LIGHTS) gsurf = gpass;
+                        r.o = r.o + (r.t * rd);
+                        const int mtl = __float_as_int(s0.w);
+                        const float4 m1 = MT(2 * mtl + 1);
+                        float af;
+                        const float prob = new_direction(rd, nrm, m1.x, m1.y, st, nd, af, hb, hb_ok);
+                        graze_next = grazing(gpass, nd);
+                        rec.put(depth, 0, af);
+                        mk = (uint32_t)mtl | (p_kind(prob) << 30);
+                        direct = v3(0.0f, 0.0f, 0.0f);
+                        li = 0;
+                        delegated = false;
+                        env_pending = ENVIS && !(m1.x > 0.0f) && !(m1.y > 0.0f);   // diffuse hit
+                        lights_next = true;
+                    }
                 }
             } else if (LIGHTS && phase == PH_SHADOW) {
                 if (r.fid < 0) {   // sampleDeltaLights :279-282 (light re-sampled: deterministic)
@@ -1326,7 +1337,7 @@ void k_trace(TraceArgs a) {
             TPT_SEC(1)
             V3 td = rd;
             bool shadow = false;
-            bool tg = false;   // the next ray leaves its face within 1e-3 of its plane (grazing())
+            bool tg = redo;   // the next ray leaves its face within 1e-3 of its plane (grazing())
             if (PAIR && lights_next && !side && li == 0 && pend < 0 && (a.n_lights > 0 || (ENVIS && env_pending))) {
                 // hand this bounce's shadow rays to the idle side lane (posted at the
                 // exchange below: origin r.o, material mk, level depth)
@@ -1580,7 +1591,7 @@ void k_trace(TraceArgs a) {
             TPT_SEC(5)
             if (ts != TS_DEAD && ts != TS_IDLE) {
                 if (!begun) {
-                    ++c_trav;
+                    if (!redo) ++c_trav;
                     trav_begin(r, to, td, shadow ? TM_ANY : ((ORDERED && phase == PH_PROBE) ? TM_EMIT : TM_CLOSEST),
                                a.boxes_finite != 0, a.emit_root, a.cull_eps, tg);
                 }
