@@ -1258,7 +1258,11 @@ void k_trace(TraceArgs a) {
 #ifdef TPT_VERIFY_CULL
         if (ts == TS_DONE && vpend) {
             vpend = false;
-            verify_ray(a, r, phase, a.mtl);
+            // (an extension hit the shading prelude will trace again -- the grazing-hit
+            // rule -- is verified after that traversal)
+            if (!(TPT_GRAZE_HIT && phase == PH_EXT && r.fin && r.fid >= 0 && a.graze &&
+                  grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)))
+                verify_ray(a, r, phase, a.mtl);
         }
 #endif
 #ifdef TPT_PROFILE_PHASES
