@@ -84,6 +84,10 @@ def parse():
                     help="1-GPU rehearsal of an N-rank run: every rank's bands of an N-way split in turn, "
                          "the step = the slowest rank's")
     ap.add_argument("--emulate-rank0-only", action="store_true", help="with --emulate-ranks: rank 0's share only")
+    ap.add_argument("--emulate-order", default="forward",
+                    help="with --emulate-ranks: the order the ranks' shares run in: forward, reverse, or a "
+                         "comma list of rank ids (a rank may repeat: its last run counts), to tell a drift with "
+                         "the position in the run from a property of the rank's share")
     ap.add_argument("--build-threads", type=int, default=-2,
                     help="host threads of the traversal-tree build (tpt_scene_set_build_threads); "
                          "-2: this process's share of the usable cores (cores / local ranks)")
@@ -109,6 +113,10 @@ def parse():
                     help="spp chunks per band set (tpt_params.pipe_chunks): 0 auto (8)")
     ap.add_argument("--flags", type=int, default=0, help="TPT_FLAG_* (2 = reference traversal order)")
     ap.add_argument("--refill", type=int, default=0, help="0 = library default")
+    ap.add_argument("--wavefront", action="store_true",
+                    help="the wavefront / ray-queue variant (TPT_FLAG_WAVEFRONT; DESIGN.md section 5 'N1')")
+    ap.add_argument("--wf-slots", type=int, default=0, help="wavefront: concurrent paths (0 = every pixel)")
+    ap.add_argument("--wf-refill", type=int, default=0, help="wavefront: traversing lanes below which a trace wave runs its pass (0 = 40)")
     ap.add_argument("--leaf-batch", type=int, default=0, help="tpt_params.leaf_batch: 0 = library default")
     ap.add_argument("--extra-streams", type=int, default=0,
                     help="diagnostic: create this many busy-once HIP streams before the scene (as a process "
@@ -374,7 +382,7 @@ def main():
         args.env = None
     if args.env == "sky":
         pt.envLight = T.EnvLight(T.procedural_sky(2048, 1024), device=dev)
-    flags = args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0)
+    flags = args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0) | (T._lib.FLAG_WAVEFRONT if args.wavefront else 0)
     emulate = args.emulate_ranks if (args.emulate_ranks > 1 and world == 1) else 0
     ranks = emulate or world
 
@@ -402,7 +410,8 @@ def main():
             st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
                                   radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
                                   refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
-                                  lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch)
+                                  lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch,
+                                  wf_slots=args.wf_slots, wf_refill=args.wf_refill)
             if world == 1:
                 return st, radiances[0]
             src = radiances if on_dev else [r.cpu() for r in radiances]   # gloo: host tensors
@@ -435,15 +444,28 @@ def main():
         """measure() on this process's band, or every emulated rank's in turn
         (the step of an N-GPU run is its slowest rank's)."""
         if not emulate:
-            return measure(scaling, rank) + ([],)
-        order = [0] if args.emulate_rank0_only else list(range(emulate))
-        per = [measure(scaling, r) for r in order]
+            return measure(scaling, rank) + ([], [])
+        if args.emulate_rank0_only:
+            order = [0]
+        elif args.emulate_order == "forward":
+            order = list(range(emulate))
+        elif args.emulate_order == "reverse":
+            order = list(range(emulate))[::-1]
+        else:
+            order = [int(v) for v in args.emulate_order.split(",")]
+            if sorted(set(order)) != list(range(emulate)):
+                raise SystemExit("--emulate-order must name every rank 0..N-1")
+        runs = [(r, measure(scaling, r)) for r in order]
+        last = {r: m for r, m in runs}   # a repeated rank: its last run
+        per = [last[r] for r in range(emulate)] if not args.emulate_rank0_only else [runs[0][1]]
         slow = max(range(len(per)), key=lambda i: per[i][0])
         tot = {k: sum(p[1][k] for p in per) for k in KEYS}
         e, _, mine, bms, frame, nfr, seeds = per[slow]
-        return e, tot, mine, bms, frame, nfr, seeds, [round(p[0] / args.steps * 1e3, 3) for p in per]
+        # per_rank_ms by rank id; run_ms in the order the shares ran
+        run_ms = [[r, round(m[0] / args.steps * 1e3, 3)] for r, m in runs]
+        return e, tot, mine, bms, frame, nfr, seeds, [round(p[0] / args.steps * 1e3, 3) for p in per], run_ms
 
-    elapsed, tot, local_tot, build_ms, frame, n_frames, seeds, per_rank_ms = measure_all(args.scaling)
+    elapsed, tot, local_tot, build_ms, frame, n_frames, seeds, per_rank_ms, run_ms = measure_all(args.scaling)
 
     def verify(frame):
         """This rank's assembled frame (weak: frame `rank`, seed + rank; strong:
@@ -464,7 +486,7 @@ def main():
 
     weak = None
     if ranks > 1 and args.scaling == "strong" and args.weak_extra:
-        we, wt, _, _, _, wnf, _, wper = measure_all("weak")
+        we, wt, _, _, _, wnf, _, wper, _ = measure_all("weak")
         weak = {"value": round(wt["traversals"] / we / 1e6, 2), "unit": "Mrays/s",
                 "ms_per_step": round(we / args.steps * 1e3, 3), "frames_per_step": wnf,
                 "step": f"{wnf} frames (seeds {args.seed}..{args.seed + wnf - 1}), each banded across {ranks} ranks"
@@ -505,6 +527,7 @@ def main():
                   "launch_schedule": ("one launch per frame" if args.pipe_sets == 1 else
                                       f"pipe_sets={args.pipe_sets}" if args.pipe_sets > 1 else "auto"),
                   "lanes_per_pixel": args.lanes_per_pixel or "auto",
+                  "variant": "wavefront (k_wf_logic + k_wf_trace)" if args.wavefront else "megakernel (k_trace)",
                   "parallelism": par}
         build = T.build_identity()
         roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms, build)
@@ -545,6 +568,7 @@ def main():
         }
         if per_rank_ms:
             out["per_rank_ms"] = per_rank_ms
+            out["emulate_run_ms"] = run_ms
         if weak is not None:
             out["weak"] = weak
         if verified is not None:

@@ -127,6 +127,10 @@ typedef struct {
      * a parked leaf (speculative leaf postponement): 2 in pair mode,
      * else 4.  Bit-identical for any value. */
     int32_t leaf_batch;
+    /* TPT_FLAG_WAVEFRONT only: concurrent paths (slots; 0 = every pixel of the call) and the
+     * traversing lanes below which a trace wave runs its pass -- finished walks out, the next
+     * queued rays in (0 = auto, 40).  Bit-identical for any values. */
+    int32_t wf_slots, wf_refill;
 } tpt_params;
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
@@ -140,6 +144,11 @@ typedef struct {
                                         percent faster, and rays whose Moller-Trumbore t is rounding noise
                                         (sliver triangles, grazing edge hits) may then find another hit
                                         than the reference (5 of ~60 G rays over the BASELINE frames) */
+#define TPT_FLAG_WAVEFRONT     0x20  /* the wavefront / ray-queue variant (DESIGN.md section 5 "N1"): a logic
+                                        kernel and a persistent trace kernel alternate per ray of every
+                                        live path, path state in device memory between them; bit-identical
+                                        to the megakernel.  lanes_per_pixel, pipe_*, spp_per_launch are
+                                        not used */
 #define TPT_FLAG_ACCUMULATE    0x4   /* progressive: continue the previous call's per-pixel streams and
                                         sums (same frame size, bands and seed); the output is the mean over
                                         all accumulated samples, bit-identical to one call with their total */

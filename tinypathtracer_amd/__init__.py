@@ -381,7 +381,8 @@ class PathTracer:
     def doTrace(self, d_scene: DeviceScene, camera: Camera, framebuffer=None, nSamplesPerPixel: int = 64,
                 seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
                 flags: int = 0, refill: int = 0, accumulate: bool = False, pipe_sets: int = 0,
-                pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0):
+                pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0, wf_slots: int = 0,
+                wf_refill: int = 0):
         """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
         or torch CUDA tensors / raw device pointers (device, int).
         accumulate=True: progressive rendering (TPT_FLAG_ACCUMULATE) -- continue
@@ -397,8 +398,9 @@ class PathTracer:
         if seed is None:
             seed = int(time.time())
         self._last_seed = seed
-        p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch, flags,
-                        refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch)
+        p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch,
+                        flags | _forced_flags(), refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch, wf_slots,
+                        wf_refill)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
         rad_p = _addr(radiance)
@@ -410,7 +412,8 @@ class PathTracer:
     def doTraceFrames(self, d_scene: DeviceScene, camera: Camera, seeds, framebuffers=None,
                       nSamplesPerPixel: int = 64, max_depth: int = 8, radiances=None, band=(16, 1, 0),
                       spp_per_launch: int = 0, flags: int = 0, refill: int = 0, accumulate: bool = False,
-                      pipe_sets: int = 0, pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0):
+                      pipe_sets: int = 0, pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0,
+                      wf_slots: int = 0, wf_refill: int = 0):
         """A batch of independent frames in one trace launch (tpt_render_frames):
         frame f is doTrace(..., seed=seeds[f]) bit for bit.  framebuffers /
         radiances: None or one buffer (or None) per frame."""
@@ -424,7 +427,8 @@ class PathTracer:
             flags |= _lib.FLAG_ACCUMULATE
         W, H = self.m_width, self.m_height
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seeds[0], band[0], band[1], band[2], spp_per_launch,
-                        flags, refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch)
+                        flags | _forced_flags(), refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch, wf_slots,
+                        wf_refill)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
 
@@ -454,6 +458,14 @@ class PathTracer:
             stats = self.doTrace(d_scene, scene.m_camera, fb, nSamplesPerPixel, seed, max_depth, rad)
         d_scene.close()
         return Frame(fb, rad, stats)
+
+
+def _forced_flags() -> int:
+    """Test knob: TPT_TEST_FORCE_FLAGS (an integer) is OR-ed into every render's
+    flags, so the whole parity suite can run through a variant, e.g.
+    TPT_TEST_FORCE_FLAGS=32 (TPT_FLAG_WAVEFRONT).  Unset in production."""
+    v = os.environ.get("TPT_TEST_FORCE_FLAGS")
+    return int(v, 0) if v else 0
 
 
 def _addr(buf):

@@ -19,6 +19,7 @@ FLAG_REF_ORDER = 0x2
 FLAG_ACCUMULATE = 0x4
 FLAG_ENV_IS = 0x8
 FLAG_APPROX_CULL = 0x10
+FLAG_WAVEFRONT = 0x20
 DESC_DELTALIGHT_LAYOUT = 0x1
 
 
@@ -58,7 +59,8 @@ class Params(C.Structure):
                 ("seed", C.c_uint64), ("band_rows", C.c_int32), ("band_count", C.c_int32),
                 ("band_index", C.c_int32), ("spp_per_launch", C.c_int32), ("flags", C.c_int32),
                 ("refill", C.c_int32), ("pipe_sets", C.c_int32), ("pipe_chunks", C.c_int32),
-                ("lanes_per_pixel", C.c_int32), ("leaf_batch", C.c_int32)]
+                ("lanes_per_pixel", C.c_int32), ("leaf_batch", C.c_int32), ("wf_slots", C.c_int32),
+                ("wf_refill", C.c_int32)]
 
 
 class Stats(C.Structure):

@@ -195,6 +195,41 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s);
 hipError_t launch_sliver_scan(const float4* tri, int32_t n, uint8_t* sliver, unsigned long long* coord_max,
                               hipStream_t s);
 
+// wavefront.hip: the wavefront / ray-queue variant (TPT_FLAG_WAVEFRONT).  The
+// queues are split into kWfShards shards (one per XCD) of shard_cap entries.  Slots
+// run pixels' sample chains; their state lives here between iterations, and the
+// rays move through two ping-pong queues (2 float4 each: origin + slot, direction
+// + flags) with one hit record (t, u, v, fid code) per queue position.
+constexpr int kWfShards = 8;
+constexpr int kWfCtlStride = 1024;                     // words between control words (4 KiB)
+constexpr int kWfCtlWords = (4 * kWfShards + 1) * kWfCtlStride;
+struct WfArgs {
+    TraceArgs t;                         // scene, camera, frame, RNG/accumulator planes, counters
+    int32_t n_slots;                     // concurrent paths (slots)
+    int32_t state_words;                 // 16, or 32 with delta lights / env IS / reference order
+    int32_t rec_words;                   // path-record words per bounce (2 or 5)
+    int32_t ordered;                     // 0: the reference's visit order (TPT_FLAG_REF_ORDER)
+    uint32_t* st0;                       // path state beside queue 0's entries: state_words per entry
+    uint32_t* st1;                       // ... beside queue 1's
+    float* rec;                          // n_slots * max_depth * rec_words
+    float4* q_ray0;                      // 2 * kWfShards * shard_cap float4
+    float4* q_ray1;                      // 2 * kWfShards * shard_cap float4
+    float4* q_hit;                       // kWfShards * shard_cap float4
+    uint32_t* ctl;                       // kWfCtlWords: shard sizes and fetch heads of both queues, claims
+    int32_t shard_cap;                   // entries per shard: ceil(n_slots / 256 / kWfShards) * 256
+    int32_t n_claims;                    // claim ids (k_trace dispatch order; those outside the band are skipped)
+    int32_t refill;                      // k_wf_trace: a wave runs its pass (hits out, rays in) below this many
+                                         //   traversing lanes
+    int32_t chunk;                       // k_wf_trace: queue entries a wave takes per global atomic
+    int32_t batch;                       // iterations enqueued between two checks of the queue size
+    int32_t logic_blocks, trace_blocks;  // grid sizes (both kernels are grid-stride / persistent)
+    int32_t it;                          // set per launch: iteration (queue it & 1 is consumed)
+    int32_t stack_lds_slots, lds_stack_offset, lds_bytes;   // set by launch_wavefront
+};
+// Runs every iteration until the queues are empty (stream-ordered; the caller
+// synchronises).  h_count: 2 * kWfShards words of pinned host memory; ev: 2 events.
+hipError_t launch_wavefront(WfArgs w, uint32_t* h_count, hipEvent_t ev[2], int32_t* iterations, hipStream_t s);
+
 // trace.hip
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);

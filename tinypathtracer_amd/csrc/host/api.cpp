@@ -400,6 +400,13 @@ struct tpt_scene {
     std::vector<hipStream_t> pipe;
     std::vector<hipEvent_t> lev;
     hipEvent_t pipe_ev[2 * kMaxPipe] = {};
+    // wavefront variant (TPT_FLAG_WAVEFRONT, wavefront.hip): slot state, path
+    // records, the two ray queues, the hit records, the control words
+    DevBuf<uint32_t> wf_state, wf_ctl;
+    DevBuf<float> wf_rec;
+    DevBuf<float4> wf_q0, wf_q1, wf_hit;
+    HostPinned<uint32_t> wf_count;
+    hipEvent_t wf_ev[2] = {nullptr, nullptr};
 
     ~tpt_scene() {
         DeviceGuard g(device);
@@ -408,6 +415,8 @@ struct tpt_scene {
         for (auto& e : lev)
             if (e) (void)hipEventDestroy(e);
         for (auto& e : pipe_ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : wf_ev)
             if (e) (void)hipEventDestroy(e);
         for (auto& q : pipe)
             if (q) (void)hipStreamDestroy(q);
@@ -1093,6 +1102,75 @@ tpt_status tpt_render(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, c
     return tpt_render_frames(s, env, cam, p, 1, &seed, &radiance_out, &bgra_out, stats);
 }
 
+// The wavefront / ray-queue variant (TPT_FLAG_WAVEFRONT; wavefront.hip, DESIGN.md
+// section 5 "N1"): every pixel's samples on one slot, in order, so the frame is
+// bit-identical to k_trace's.  Slots default to every pixel of the call (the
+// whole frame in flight: the fewest iterations); the buffers stay with the
+// scene between calls.  The trace phase runs on the scene's stream after the
+// RNG initialisation (event ev[1]).
+static tpt_status render_wavefront(tpt_scene* s, const tpt::TraceArgs& a, const tpt_params* p, int n_frames, int bh,
+                                   double& trace_ms, double& kernel_ms, int& launches) {
+    hipStream_t st = s->stream;
+    const bool ordered = !(p->flags & TPT_FLAG_REF_ORDER);
+    // the megakernel's record layout: 5 words with delta lights, env IS or the reference order
+    const bool lights = !ordered || a.env_is || tpt::rec_words(s->n_lights, s->n_materials) == 5;
+    tpt::WfArgs w{};
+    w.t = a;
+    w.t.samples = p->spp;
+    w.ordered = ordered ? 1 : 0;
+    w.state_words = lights ? 32 : 16;
+    w.rec_words = lights ? 5 : 2;
+    const size_t gx = (size_t)(p->width + 15) / 16, gy = (size_t)((bh + 15) / 16) * (size_t)n_frames;
+    const size_t claims = gx * gy * 256;
+    if (bh <= 0) return TPT_OK;
+    if (claims > (size_t)INT32_MAX / 2) return fail(TPT_ERR_INVALID_ARG, "wavefront: frame batch too large");
+    if (p->wf_slots < 0 || p->wf_refill < 0 || p->wf_refill > 64)
+        return fail(TPT_ERR_INVALID_ARG, "wavefront: wf_slots >= 0, wf_refill 0..64");
+    size_t slots = p->wf_slots > 0 ? (size_t)p->wf_slots : claims;
+    slots = std::min(slots, claims);
+    slots = (slots + 255) / 256 * 256;
+    w.n_claims = (int32_t)claims;
+    w.n_slots = (int32_t)slots;
+    HIP_OR_FAIL(s->wf_rec.alloc(slots * (size_t)p->max_depth * (size_t)w.rec_words));
+    // queue shards: a logic block appends to shard blockIdx % kWfShards, and the grid
+    // (a multiple of kWfShards) deals 256-entry chunks round-robin, so a shard
+    // receives at most every kWfShards-th chunk of a queue of <= slots entries
+    const size_t cap = ((slots / 256) + tpt::kWfShards - 1) / tpt::kWfShards * 256;
+    const size_t qn = cap * tpt::kWfShards;
+    HIP_OR_FAIL(s->wf_q0.alloc(2 * qn));
+    HIP_OR_FAIL(s->wf_q1.alloc(2 * qn));
+    HIP_OR_FAIL(s->wf_hit.alloc(qn));
+    HIP_OR_FAIL(s->wf_state.alloc(2 * qn * (size_t)w.state_words));
+    HIP_OR_FAIL(s->wf_ctl.alloc(tpt::kWfCtlWords));
+    HIP_OR_FAIL(s->wf_count.alloc(2 * tpt::kWfShards));
+    w.shard_cap = (int32_t)cap;
+    for (auto& e : s->wf_ev)
+        if (!e) HIP_OR_FAIL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    w.st0 = s->wf_state.p;
+    w.st1 = s->wf_state.p + qn * (size_t)w.state_words;
+    w.rec = s->wf_rec.p;
+    w.q_ray0 = s->wf_q0.p;
+    w.q_ray1 = s->wf_q1.p;
+    w.q_hit = s->wf_hit.p;
+    w.ctl = s->wf_ctl.p;
+    w.refill = p->wf_refill > 0 ? p->wf_refill : 40;
+    w.chunk = 128;
+    w.batch = 32;
+    w.logic_blocks = (int32_t)((std::min<size_t>((slots + 255) / 256, 2048) + tpt::kWfShards - 1) / tpt::kWfShards *
+                               tpt::kWfShards);
+    w.trace_blocks = 0;   // launch_wavefront: the CUs' occupancy
+    int32_t iters = 0;
+    HIP_OR_FAIL(tpt::launch_wavefront(w, s->wf_count.p, s->wf_ev, &iters, st));
+    HIP_OR_FAIL(hipEventRecord(s->ev[2], st));
+    HIP_OR_FAIL(hipEventSynchronize(s->ev[2]));
+    float ms = 0.0f;
+    HIP_OR_FAIL(hipEventElapsedTime(&ms, s->ev[1], s->ev[2]));
+    trace_ms = ms;
+    kernel_ms = ms;
+    launches = 1 + 2 * iters;
+    return TPT_OK;
+}
+
 tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, const tpt_params* p,
                              int32_t n_frames, const uint64_t* seeds, float* const* radiance_outs,
                              uint8_t* const* bgra_outs, tpt_stats* stats) {
@@ -1237,6 +1315,14 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // between chunks), so the result is bit-identical to one launch.
     // params pipe_sets (1: one stream) and pipe_chunks (chunks per set) override;
     // an explicit spp_per_launch keeps the single-stream chunked loop.
+    double trace_ms = 0.0, kernel_ms = 0.0;
+    int launches = 0;
+    const char* dbg_path = nullptr;
+    size_t dbg_words = 0;
+    if (p->flags & TPT_FLAG_WAVEFRONT) {   // the wavefront / ray-queue variant (wavefront.hip)
+        const tpt_status ws = render_wavefront(s, a, p, n_frames, bh, trace_ms, kernel_ms, launches);
+        if (ws != TPT_OK) return ws;
+    } else {
     int chunk = p->spp_per_launch;
     int nset = 1;
     if (chunk <= 0) {
@@ -1279,14 +1365,12 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     a.debug_waves = nullptr;
 #if defined(TPT_PROFILE_PHASES) || defined(TPT_VERIFY_CULL)
     // per-wave dump (phase-profiling builds) / traversal mismatch log (cull-verification builds)
-    const char* dbg_path = std::getenv("TPT_DEBUG_WAVES");
-#else
-    const char* dbg_path = nullptr;
+    dbg_path = std::getenv("TPT_DEBUG_WAVES");
 #endif
     // one record per wave of the largest grid (pair mode: 16x8-pixel workgroups)
     const size_t dbg_launch =
         8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 7) / 8) * nf;
-    const size_t dbg_words = dbg_launch * std::max<size_t>(plan.size(), 1);   // one region per launch
+    dbg_words = dbg_launch * std::max<size_t>(plan.size(), 1);   // one region per launch
     if (dbg_path) {
         HIP_OR_FAIL(s->debug.alloc(dbg_words));
         HIP_OR_FAIL(hipMemsetAsync(s->debug.p, 0, dbg_words * sizeof(unsigned long long), st));
@@ -1358,8 +1442,6 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     SET_OR_FAIL(hipEventRecord(s->ev[2], st));   // end of the trace phase
     SET_OR_FAIL(hipEventSynchronize(s->ev[2]));
 #undef SET_OR_FAIL
-    double trace_ms = 0.0, kernel_ms = 0.0;
-    int launches = 0;
     {
         float ms = 0.0f;
         HIP_OR_FAIL(hipEventElapsedTime(&ms, s->ev[1], s->ev[2]));
@@ -1371,6 +1453,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
             ++launches;
         }
     }
+    }   // launch plan (k_trace)
 
     // copyToFB (:553) + radiance readout, per frame
     HIP_OR_FAIL(hipEventRecord(s->ev[2], st));

@@ -6,7 +6,7 @@
 # each bench JSON is kept as gpurun_out/abn_<cfg>_<variant>_<rep>.json.
 set -o pipefail
 export TMPDIR=/tmp
-CFGS=${1:-C2}; VARS=${2:-"cur r03"}; REPS=${3:-2}; shift 3; EXTRA="$@"
+CFGS=${1:-C2}; VARS=${2:-"cur r03"}; REPS=${3:-2}; shift $(( $# < 3 ? $# : 3 )); EXTRA="$@"
 mkdir -p gpurun_out
 for rep in $(seq $REPS); do
 for v in $VARS; do

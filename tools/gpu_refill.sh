@@ -3,7 +3,7 @@
 # Usage: bash tools/gpu_refill.sh CFG "R1 R2 .." [reps] [extra bench args]
 set -o pipefail
 export TMPDIR=/tmp
-CFG=${1:-C2}; RS=${2:-"16 24"}; REPS=${3:-1}; shift 3; EXTRA="$@"
+CFG=${1:-C2}; RS=${2:-"16 24"}; REPS=${3:-1}; shift $(( $# < 3 ? $# : 3 )); EXTRA="$@"
 mkdir -p gpurun_out
 for rep in $(seq $REPS); do
 for r in $RS; do
