@@ -80,6 +80,10 @@ def parse():
                          "weak: N frames per step, each banded across the N ranks (all-to-all)")
     ap.add_argument("--weak-extra", type=int, default=1,
                     help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
+    ap.add_argument("--fast-extra", type=int, default=1,
+                    help="1 GPU: also time the tolerance mode (TPT_FLAG_FAST: FMA contraction, hardware "
+                         "rcp/sqrt/sin/cos, no culling guards; images within SURVEY 8(d)'s tolerance, not bit-exact) "
+                         "and report it under the key 'tolerance_mode' beside the exact headline")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of an N-rank run: every rank's bands of an N-way split in turn, "
                          "the step = the slowest rank's")
@@ -391,7 +395,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    def measure(scaling, band_index):
+    def measure(scaling, band_index, extra_flags=0):
         """Warm-up + K timed steps of one scaling mode with this process
         rendering band `band_index` of `ranks`; returns (max-over-ranks
         elapsed, summed stats over ranks, this rank's stats, build ms, the last
@@ -408,7 +412,8 @@ def main():
             d_scene.build(asynchronous=bool(args.async_build))
             build_ms.append((time.perf_counter() - tb) * 1e3)
             st = pt.doTraceFrames(d_scene, scene.m_camera, seeds, None, args.spp, max_depth=args.depth,
-                                  radiances=radiances, band=band, spp_per_launch=args.spp_per_launch, flags=flags,
+                                  radiances=radiances, band=band, spp_per_launch=args.spp_per_launch,
+                                  flags=flags | extra_flags,
                                   refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
                                   lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch,
                                   wf_slots=args.wf_slots, wf_refill=args.wf_refill)
@@ -495,6 +500,16 @@ def main():
         if wper:
             weak["per_rank_ms"] = wper
 
+    tolerance = None
+    if world == 1 and not emulate and args.fast_extra and not args.wavefront:
+        fe, ft, _, _, _, _, _ = measure(args.scaling, 0, T._lib.FLAG_FAST)
+        tolerance = {"value": round(ft["traversals"] / fe / 1e6, 2), "unit": "Mrays/s",
+                     "ms_per_step": round(fe / args.steps * 1e3, 3), "flags": "TPT_FLAG_FAST",
+                     "what": "tolerance mode: FMA contraction and FMA slab tests, hardware rcp/sqrt/sin/cos, no "
+                             "culling guards; images within SURVEY 8(d)'s per-channel tolerance of the reference "
+                             "(tests/test_gpu_tolerance.py, test_gpu_fullsize.py mode fast), not bit-exact",
+                     "vs_exact": None}
+
     if rank == 0:
         K = args.steps
         rays = tot["traversals"]
@@ -571,6 +586,9 @@ def main():
             out["emulate_run_ms"] = run_ms
         if weak is not None:
             out["weak"] = weak
+        if tolerance is not None:
+            tolerance["vs_exact"] = round(tolerance["value"] / value, 4)
+            out["tolerance_mode"] = tolerance
         if verified is not None:
             # the assembled frame(s) must equal one GPU rendering every row (the
             # RNG subsequence is the global pixel index, path_tracer.cu:39,320)

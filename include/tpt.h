@@ -149,6 +149,12 @@ typedef struct {
                                         live path, path state in device memory between them; bit-identical
                                         to the megakernel.  lanes_per_pixel, pipe_*, spp_per_launch are
                                         not used */
+#define TPT_FLAG_FAST          0x40  /* tolerance mode: the trace kernel built with FMA
+                                        contraction, FMA slab tests and the hardware's approximate reciprocal,
+                                        sqrt, sin and cos, without the culling guards (implies
+                                        TPT_FLAG_APPROX_CULL).  Images match the reference within SURVEY
+                                        8(d)'s tolerance (mean |d| <= 1e-3, p99 <= 1e-2, >= 99.5 % of pixels
+                                        within one 8-bit step), not bit for bit.  Not with TPT_FLAG_WAVEFRONT */
 #define TPT_FLAG_ACCUMULATE    0x4   /* progressive: continue the previous call's per-pixel streams and
                                         sums (same frame size, bands and seed); the output is the mean over
                                         all accumulated samples, bit-identical to one call with their total */

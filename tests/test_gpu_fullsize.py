@@ -142,15 +142,32 @@ ORACLE_BAND = [
 ]
 
 
+_ORACLE_BANDS = {}
+
+
+def _oracle_band(cfg, name, W, H, spp, depth, sky, env_is, band):
+    """The oracle's render of the middle band at full spp, once per config (the
+    exact and the tolerance-mode tests share it)."""
+    from oracle import oracle as O
+    if cfg not in _ORACLE_BANDS:
+        _ORACLE_BANDS[cfg] = O.render(O.load_scene(scene_path(name)), W, H, spp, depth, 42,
+                                      env=sky[::-1].copy() if sky is not None else None, trig_mode=1,
+                                      band_rows=band[0], band_count=band[1], band_index=band[2], env_is=env_is)
+    return _ORACLE_BANDS[cfg]
+
+
+@pytest.mark.parametrize("mode", ["exact", "fast"])
 @pytest.mark.parametrize("cfg,name,W,H,spp,depth,env,env_is", ORACLE_BAND)
-def test_full_spp_band_matches_oracle(cfg, name, W, H, spp, depth, env, env_is):
+def test_full_spp_band_matches_oracle(cfg, name, W, H, spp, depth, env, env_is, mode):
     """Every BASELINE configuration at its FULL spp against the CPU oracle
     (not only against the GPU's own reference order): one 16-row band through
     the middle of the frame (the heaviest rows; band = the multi-GPU band
     decomposition, row y in band (y // 16) % count), rendered by both with the
-    same seed -- every pixel's radiance bit for bit, the framebuffer bytes and
-    the ray count equal."""
-    from oracle import oracle as O
+    same seed.  exact: every pixel's radiance bit for bit, the ray count equal.
+    fast (TPT_FLAG_FAST, tolerance mode): SURVEY 8(d)'s per-channel tolerance --
+    mean |d| <= 1e-3, p99 |d| <= 1e-2, >= 99.5 % of pixels within one 8-bit step
+    -- and the ray count within 1 %."""
+    from tests.test_gpu_parity import assert_parity, image_metrics
     count = (H + 15) // 16
     band = (16, count, count // 2)
     s = T.Scene(scene_path(name))
@@ -160,17 +177,21 @@ def test_full_spp_band_matches_oracle(cfg, name, W, H, spp, depth, env, env_is):
         pt = T.PathTracer("", W, H, 0)
         if env:
             pt.envLight = T.EnvLight(sky, 0)
-        flags = T._lib.FLAG_ENV_IS if env_is else 0
+        flags = (T._lib.FLAG_ENV_IS if env_is else 0) | (T._lib.FLAG_FAST if mode == "fast" else 0)
         rad = np.zeros((H, W, 3), np.float32)
         st = pt.doTrace(d, s.m_camera, None, spp, seed=42, max_depth=depth, radiance=rad, band=band, flags=flags)
-        orad, _, oc = O.render(O.load_scene(scene_path(name)), W, H, spp, depth, 42,
-                               env=sky[::-1].copy() if env else None, trig_mode=1, band_rows=band[0],
-                               band_count=band[1], band_index=band[2], env_is=env_is)
+        orad, _, oc = _oracle_band(cfg, name, W, H, spp, depth, sky, env_is, band)
         rows = np.array([(y // 16) % count == band[2] for y in range(H)])
         assert rows.sum() == 16
-        diff = int((_bits(rad[rows]) != _bits(orad[rows])).any(-1).sum())
-        assert diff == 0, (cfg, diff)
-        assert st["traversals"] == oc["traversals"], cfg
+        if mode == "exact":
+            diff = int((_bits(rad[rows]) != _bits(orad[rows])).any(-1).sum())
+            assert diff == 0, (cfg, diff)
+            assert st["traversals"] == oc["traversals"], cfg
+        else:
+            m = image_metrics(rad[rows], orad[rows])
+            print(cfg, "tolerance mode", m)
+            assert_parity(m, bit_min=0.0)
+            assert abs(st["traversals"] - oc["traversals"]) <= 0.01 * oc["traversals"], cfg
         assert rad[rows].max() > 0.0
     finally:
         d.close()

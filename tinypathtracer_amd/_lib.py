@@ -20,6 +20,7 @@ FLAG_ACCUMULATE = 0x4
 FLAG_ENV_IS = 0x8
 FLAG_APPROX_CULL = 0x10
 FLAG_WAVEFRONT = 0x20
+FLAG_FAST = 0x40
 DESC_DELTALIGHT_LAYOUT = 0x1
 
 

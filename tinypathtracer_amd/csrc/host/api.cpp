@@ -1233,7 +1233,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     a.n_frames = n_frames;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
-    if (p->flags & TPT_FLAG_APPROX_CULL) {   // culls without the exactness guards (trace.hip "Culling")
+    if (p->flags & (TPT_FLAG_APPROX_CULL | TPT_FLAG_FAST)) {   // culls without the exactness guards (trace.hip "Culling")
         a.cull_eps = 0.0f;
         a.n_sliver_groups = 0;
         a.graze = 0;
@@ -1319,6 +1319,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     int launches = 0;
     const char* dbg_path = nullptr;
     size_t dbg_words = 0;
+    if ((p->flags & TPT_FLAG_WAVEFRONT) && (p->flags & (TPT_FLAG_FAST | TPT_FLAG_APPROX_CULL)))
+        return fail(TPT_ERR_INVALID_ARG, "TPT_FLAG_WAVEFRONT runs the exact traversal only");
     if (p->flags & TPT_FLAG_WAVEFRONT) {   // the wavefront / ray-queue variant (wavefront.hip)
         const tpt_status ws = render_wavefront(s, a, p, n_frames, bh, trace_ms, kernel_ms, launches);
         if (ws != TPT_OK) return ws;
@@ -1432,7 +1434,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         if (dbg_path) ak.debug_waves = s->debug.p + oi * dbg_launch;
 #endif
         SET_OR_FAIL(hipEventRecord(s->lev[2 * j], qs[k]));
-        SET_OR_FAIL(tpt::launch_trace(ak, qs[k]));
+        SET_OR_FAIL((p->flags & TPT_FLAG_FAST) ? tpt_fast::launch_trace_ptr(&ak, qs[k]) : tpt::launch_trace(ak, qs[k]));
         SET_OR_FAIL(hipEventRecord(s->lev[2 * j + 1], qs[k]));
     }
     for (int k = 0; nset > 1 && k < nset; ++k) {   // join

@@ -1253,6 +1253,10 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The host calls the tolerance-mode build (namespace tpt_fast, the same TraceArgs
+// layout) through this entry point.
+hipError_t launch_trace_ptr(const void* a, hipStream_t s) { return launch_trace(*static_cast<const TraceArgs*>(a), s); }
+
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s) {
     dim3 grid((a.width + 255) / 256, a.band_height);
     hipLaunchKernelGGL(k_resolve, grid, dim3(256), 0, s, a);

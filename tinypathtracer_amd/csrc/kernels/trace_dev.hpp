@@ -15,6 +15,14 @@
 #include "../common/tpt_math.hpp"
 #include "tpt.h"
 
+#ifndef TPT_FAST
+// 1: the tolerance-mode build of this file (Makefile trace_fast.hip.o, namespace
+// tpt_fast, TPT_FLAG_FAST; DESIGN.md section 4 "Tolerance mode"): FMA
+// contraction, FMA slab tests, the hardware's approximate reciprocal, sqrt and
+// sin/cos, no culling guards.  The images then match the reference within SURVEY
+// 8(d)'s per-channel tolerance, not bit for bit.
+#define TPT_FAST 0
+#endif
 #ifndef TPT_PROBE_SHORTCUT
 #define TPT_PROBE_SHORTCUT 1   // no emissive triangle: resolve direct probes in the shading pass
 #endif
@@ -201,7 +209,10 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
                                            int emit_root = -1, float cull_eps = 0.0f, bool graze = false) {
     r.o = o;
     r.d = d;
-    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
+    if (TPT_FAST)
+        r.inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    else
+        r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
     r.node = 0;
     r.sp = 0;
     r.pend = -1;
@@ -282,9 +293,18 @@ __device__ __forceinline__ void inner_visit(const Trav& r, const float4* __restr
 // differ from the ternaries; only comparisons consume T0/T1.
 __device__ __forceinline__ void slab_minmax(const V3& o, const V3& inv, float nx, float ny, float nz, float xx,
                                             float xy, float xz, float& t0, float& t1) {
+#if TPT_FAST
+    // (n - o) / d as one FMA per bound: n * (1/d) - o * (1/d) (the o * (1/d) terms
+    // are common to every box a visit tests)
+    const float ox = -(o.x * inv.x), oy = -(o.y * inv.y), oz = -(o.z * inv.z);
+    const float ax = __builtin_fmaf(nx, inv.x, ox), bx = __builtin_fmaf(xx, inv.x, ox);
+    const float ay = __builtin_fmaf(ny, inv.y, oy), by = __builtin_fmaf(xy, inv.y, oy);
+    const float az = __builtin_fmaf(nz, inv.z, oz), bz = __builtin_fmaf(xz, inv.z, oz);
+#else
     const float ax = (nx - o.x) * inv.x, bx = (xx - o.x) * inv.x;
     const float ay = (ny - o.y) * inv.y, by = (xy - o.y) * inv.y;
     const float az = (nz - o.z) * inv.z, bz = (xz - o.z) * inv.z;
+#endif
     t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
     t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
 }
@@ -432,7 +452,7 @@ __device__ __forceinline__ bool tri_core(const V3& o, const V3& d, const V3& v0,
     const V3 p = cross(d, e2);
     const V3 q = cross(tv, e1);
     const float denom = dot(p, e1);
-    const float id = 1.0f / denom;
+    const float id = TPT_FAST ? __builtin_amdgcn_rcpf(denom) : 1.0f / denom;
     u = dot(p, tv) * id;
     v = dot(q, d) * id;
     t = dot(q, e2) * id;
@@ -714,11 +734,20 @@ __device__ __forceinline__ float new_direction(V3 d, V3 n, float eta_m, float me
     const V3 xb = hb.xb;
     // HemisphereCosine (sampler.h:75-89)
     const V3 zb = cross(xb, n);
+    float sp, cp;
+#if TPT_FAST
+    // v_sin_f32 / v_cos_f32 take revolutions: sin(2 pi u) directly
+    const float u_phi = xorwow_uniform(st);
+    const float cos_t = __builtin_amdgcn_sqrtf(xorwow_uniform(st));
+    const float sin_t = __builtin_amdgcn_sqrtf(1.0f - cos_t * cos_t);
+    sp = __builtin_amdgcn_sinf(u_phi);
+    cp = __builtin_amdgcn_cosf(u_phi);
+#else
     const float phi = 2.0f * kPi * xorwow_uniform(st);
     const float cos_t = fsqrt(xorwow_uniform(st));
     const float sin_t = fsqrt(1.0f - cos_t * cos_t);
-    float sp, cp;
     fsincos_2pi(phi, sp, cp);
+#endif
     const float x = cp * sin_t;
     const float z = sp * sin_t;
     next = ((x * xb) + (cos_t * n)) + (z * zb);
