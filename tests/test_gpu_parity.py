@@ -23,6 +23,12 @@ pytestmark = pytest.mark.gpu
 SCENES = ["box", "box1", "box2", "ball", "tir", "light", "square", "c5"]
 
 
+# TPT_TEST_FORCE_FLAGS (tinypathtracer_amd._forced_flags) runs the suite through a
+# variant; the wavefront variant has its own launch schedule, so the assertions
+# on k_trace's launch counts do not apply to it (the images still must match)
+FORCED_WAVEFRONT = bool(int(os.environ.get("TPT_TEST_FORCE_FLAGS", "0"), 0) & T._lib.FLAG_WAVEFRONT)
+
+
 def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
@@ -228,7 +234,7 @@ def test_render_parity_full_resolution(built, name, W, H, spp, depth, env):
         assert np.array_equal(fb[..., :3], obgra[..., :3]), label
         assert st["traversals"] == oc["traversals"], label
         assert st["shade_hits"] == oc["shade_hits"], label
-        if label == "pipeline":
+        if label == "pipeline" and not FORCED_WAVEFRONT:
             assert st["trace_launches"] > 3
 
 
@@ -370,7 +376,7 @@ def test_frame_batch_bit_identical(built):
     rads = [np.zeros((H, W, 3), np.float32) for _ in seeds]
     fbo = [np.zeros((H, W, 4), np.uint8) for _ in seeds]
     st = pt.doTraceFrames(d, s.m_camera, seeds, fbo, spp, radiances=rads)
-    assert st["trace_launches"] == 1 and st["pixels"] == W * H * len(seeds)
+    assert (FORCED_WAVEFRONT or st["trace_launches"] == 1) and st["pixels"] == W * H * len(seeds)
     for f in range(len(seeds)):
         assert np.array_equal(_bits(rads[f]), _bits(singles[f])), f
         assert np.array_equal(fbo[f], fbs[f]), f
@@ -397,7 +403,7 @@ def test_spp_chunking_bit_identical(built):
     b = np.zeros((H, W, 3), np.float32)
     pt.doTrace(d, s.m_camera, None, spp, seed=9, radiance=a, spp_per_launch=spp)
     st = pt.doTrace(d, s.m_camera, None, spp, seed=9, radiance=b, spp_per_launch=5)
-    assert st["trace_launches"] == 3
+    assert FORCED_WAVEFRONT or st["trace_launches"] == 3
     assert np.array_equal(_bits(a), _bits(b))
 
 
@@ -412,7 +418,7 @@ def test_launch_pipeline_bit_identical(built):
     one = np.zeros((H, W, 3), np.float32)
     fb1 = np.zeros((H, W, 4), np.uint8)
     st1 = pt.doTrace(d, s.m_camera, fb1, spp, seed=11, radiance=one, pipe_sets=1)
-    assert st1["trace_launches"] == 1
+    assert FORCED_WAVEFRONT or st1["trace_launches"] == 1
     seeds = [11, 12]
     batch1 = [np.zeros((H, W, 3), np.float32) for _ in seeds]
     pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch1, pipe_sets=1)
@@ -420,7 +426,7 @@ def test_launch_pipeline_bit_identical(built):
         got = np.zeros((H, W, 3), np.float32)
         fb = np.zeros((H, W, 4), np.uint8)
         st = pt.doTrace(d, s.m_camera, fb, spp, seed=11, radiance=got, pipe_sets=sets)
-        assert st["trace_launches"] == launches, sets
+        assert FORCED_WAVEFRONT or st["trace_launches"] == launches, sets
         assert st["traversals"] == st1["traversals"]
         assert st["trace_kernel_ms"] > 0.0
         assert np.array_equal(_bits(got), _bits(one)), sets
@@ -435,7 +441,7 @@ def test_launch_pipeline_bit_identical(built):
     assert np.array_equal(_bits(banded), _bits(one))
     batch = [np.zeros((H, W, 3), np.float32) for _ in seeds]
     st = pt.doTraceFrames(d, s.m_camera, seeds, None, spp, radiances=batch, pipe_sets=2)
-    assert st["trace_launches"] > 1
+    assert FORCED_WAVEFRONT or st["trace_launches"] > 1
     for f in range(len(seeds)):
         assert np.array_equal(_bits(batch[f]), _bits(batch1[f])), f
 

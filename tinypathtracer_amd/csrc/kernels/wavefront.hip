@@ -651,7 +651,10 @@ static void launch_logic(const WfArgs& w, int init, hipStream_t s) {
 }
 static void wf_logic(const WfArgs& w, int init, hipStream_t s) {
     const bool lights = w.state_words == 32;
-    if (!w.ordered) launch_logic<false, true, false>(w, init, s);
+    if (!w.ordered) {
+        if (w.t.env_is) launch_logic<false, true, true>(w, init, s);
+        else launch_logic<false, true, false>(w, init, s);
+    }
     else if (w.t.env_is) launch_logic<true, true, true>(w, init, s);
     else if (lights) launch_logic<true, true, false>(w, init, s);
     else launch_logic<true, false, false>(w, init, s);
