@@ -157,6 +157,12 @@ def scene_file(name):
         out = os.path.join(tempfile.gettempdir(), "tpt_scenes", "c5.gltf")
         synth.write_c5(out, SCENE_DIR)
         return out
+    if name.startswith("x1s") or name in ("x2", "x3"):   # the exactness scenes (synth.exactness_scene)
+        import tempfile
+        from tinypathtracer_amd import synth
+        out = os.path.join(tempfile.gettempdir(), "tpt_scenes", f"{name}.gltf")
+        synth.write_scene(synth.exactness_scene(name, SCENE_DIR), out)
+        return out
     p = os.path.join(SCENE_DIR, f"{name}.gltf")
     if not os.path.exists(p):
         p = name

@@ -188,6 +188,8 @@ def build_bvh(ps: PackedScene):
     keys = np.zeros(nf, np.int64)
     rc = lib().orc_build_bvh(nf, _ptr(wv, C.c_float), _ptr(ps.indices, C.c_uint32), nodes,
                              _ptr(keys, C.c_int64))
+    if rc == -3:
+        raise ValueError("LBVH topology invalid: a parent chain misses the root (duplicate Morton keys)")
     assert rc == 0
     arr = np.frombuffer(nodes, dtype=np.dtype([("parent", "<u4"), ("a", "<i4"), ("b", "<i4"),
                                                ("bmin", "<f4", 3), ("bmax", "<f4", 3)])).copy()

@@ -409,6 +409,14 @@ int orc_build_bvh(uint32_t nf, const float* wv, const uint32_t* idx, orc_node* n
             else              { nodes[sp].parent = (uint32_t)i;      nodes[i].b = sp; }
         }
     }
+    /* a parent chain that does not reach the root (runs of duplicate keys split
+     * without a tie-break: a cycle) -- the library refuses it too (build.hip
+     * kMaxLbvhDepth); the recursive union would not terminate */
+    for (int i = 1; i < 2 * n - 1; ++i) {
+        int cur = i, d = 0;
+        while (cur != 0 && d < 4096) { cur = (int)nodes[cur].parent; ++d; }
+        if (d >= 4096) { free(kf); free(tmp); return -3; }
+    }
     if (n_int > 0) union_box(nodes, 0, n_int);
     free(kf);
     free(tmp);
@@ -920,7 +928,13 @@ int orc_render(const orc_scene* s, const orc_env* env, const orc_camera* cam, co
     memset(wv, 0, sizeof(float) * 3 * nv);
     memset(wn, 0, sizeof(float) * 3 * nv);
     orc_transform(s, wv, wn);
-    orc_build_bvh((uint32_t)nf, wv, s->indices, nodes, keys);
+    {
+        const int brc = orc_build_bvh((uint32_t)nf, wv, s->indices, nodes, keys);
+        if (brc != 0) {
+            free(wv); free(wn); free(nodes); free(keys); free(states);
+            return brc;
+        }
+    }
 
     trace_ctx c;
     c.b.nodes = nodes; c.b.wv = wv; c.b.wn = wn; c.b.idx = s->indices; c.b.n_faces = (int)nf;

@@ -26,6 +26,12 @@ def scene_path(name):
         out = os.path.join(tempfile.gettempdir(), "tpt_scenes", "c5.gltf")
         synth.write_c5(out, SCENE_DIR)
         return out
+    if name.startswith("x1s") or name in ("x2", "x3"):   # exactness scenes (synth.exactness_scene)
+        import tempfile
+        from tinypathtracer_amd import synth
+        out = os.path.join(tempfile.gettempdir(), "tpt_scenes", f"{name}.gltf")
+        synth.write_scene(synth.exactness_scene(name, SCENE_DIR), out)
+        return out
     return os.path.join(SCENE_DIR, f"{name}.gltf")
 
 

@@ -48,3 +48,27 @@ def test_subdivision_is_watertight_and_unit_normals():
     hits = [i for i in range(len(P)) if np.array_equal(P[i].view(np.uint32), m12_a.view(np.uint32))]
     assert len(hits) >= 4   # each child touching the edge carries the identical vertex
     assert np.allclose(np.linalg.norm(N, axis=1), 1.0, atol=1e-6)
+
+
+def test_exactness_scenes_deterministic_and_loader_parity(tmp_path):
+    """The exactness scenes (synth.exactness_scene; tests/test_gpu_exactness_scenes.py):
+    the same bytes every time, and the native loader reads them as the oracle's does."""
+    import pytest
+    from oracle import oracle as O
+    for k in ("x1s1", "x1s2", "x3"):
+        d1 = synth.write_scene(synth.exactness_scene(k, SCENE_DIR), str(tmp_path / f"{k}a.gltf"))
+        d2 = synth.write_scene(synth.exactness_scene(k, SCENE_DIR), str(tmp_path / f"{k}b.gltf"))
+        assert d1 == d2
+        p = scene_path(k)
+        a, b = T.Scene(p), S.load_gltf(p)
+        u = lambda x: np.ascontiguousarray(x, np.float32).view(np.uint32)
+        assert np.array_equal(a.indices, b.indices)
+        assert np.array_equal(u(a.vertices), u(b.vertices))
+        assert np.array_equal(u(a.vert_trans), u(b.vert_trans))
+        assert np.array_equal(u(a.normal_trans), u(b.normal_trans))
+        O.build_bvh(O.load_scene(p))   # a valid LBVH topology
+    assert T.Scene(scene_path("x1s1")).n_faces == 31600
+    # x2 stacks three boxes exactly: the reference's LBVH (computeNodeRange without a
+    # tie-break on duplicate keys) leaves a parent chain that misses the root
+    with pytest.raises(ValueError, match="topology invalid"):
+        O.build_bvh(O.load_scene(scene_path("x2")))

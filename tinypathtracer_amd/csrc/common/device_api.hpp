@@ -186,6 +186,9 @@ struct BuildBuffers {
     uint32_t out_boxes_finite;           // 1: every inner-node child box is finite
     uint32_t out_n4;                     // 4-wide nodes (breadth-first prefix of inner4)
 };
+// launch_build fails with hipErrorInvalidValue (out_max_depth >= kMaxLbvhDepth)
+// when a leaf's parent chain does not reach the root within this many steps
+constexpr uint32_t kMaxLbvhDepth = 4096;
 hipError_t build_sort_tmp_bytes(int32_t n, size_t* bytes);
 hipError_t launch_build(BuildBuffers& b, hipStream_t s);
 // Culling exactness inputs (trace.hip "Culling"), per leaf position of the packed

@@ -781,7 +781,14 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
     b.tri = s->tri.p;
     b.shade = s->shade.p;
     b.nodes36 = s->nodes36.p;
-    HIP_OR_FAIL(tpt::launch_build(b, s->stream));
+    {
+        const hipError_t be = tpt::launch_build(b, s->stream);
+        if (be != hipSuccess && b.out_max_depth >= tpt::kMaxLbvhDepth)
+            return fail(TPT_ERR_INVALID_ARG,
+                        "LBVH topology invalid: duplicate Morton keys made a node's parent chain miss the root "
+                        "(computeNodeRange, bvh.cu:150-217, has no tie-break; the reference would not terminate)");
+        HIP_OR_FAIL(be);
+    }
     s->tree_depth = b.out_max_depth;
     s->boxes_finite = (int32_t)b.out_boxes_finite;
     s->n4 = (int32_t)b.out_n4;

@@ -167,7 +167,7 @@ __global__ void k_depth(BuildBuffers b, uint32_t* depth) {
     }
     uint32_t d = 0;
     int cur = id;
-    while (cur != 0 && d < 4096) {
+    while (cur != 0 && d < kMaxLbvhDepth) {
         cur = (int)b.parent[cur];
         ++d;
     }
@@ -414,6 +414,13 @@ hipError_t launch_build(BuildBuffers& b, hipStream_t s) {
     TPT_TRY(hipMemcpyAsync(&maxd, b.max_depth, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     TPT_TRY(hipStreamSynchronize(s));
     b.out_max_depth = maxd;
+    // k_depth stops a parent walk at kMaxLbvhDepth steps: only a parent chain that
+    // never reaches the root gets there -- runs of duplicate Morton keys, which
+    // computeNodeRange (bvh.cu:150-217) splits without an index tie-break, can
+    // produce a node claimed by two parents and a cycle (the reference's own
+    // undefined behaviour: its computeBBox and traversal would not terminate).
+    // Refuse such a topology before any kernel walks it.
+    if (maxd >= kMaxLbvhDepth) return hipErrorInvalidValue;
     // internal nodes live at depth <= maxd - 1; deepest first
     for (int level = (int)maxd - 1; level >= 0 && n > 1; --level) {
         hipLaunchKernelGGL(k_union_level, grid(n - 1), blk, 0, s, b, depth, (uint32_t)level);

@@ -989,9 +989,13 @@ __global__ __launch_bounds__(256) void k_trace_rays(TraceArgs a, uint32_t n, con
             if (mode == 3 && probe_misses_emitters(a, ro, rdir)) r.node = -1;   // the render's probe pre-test
             trav_lane<true>(r, a, stk, c_ovf);
             if (a.n_sliver_groups > 0) sliver_pass(r, a, c_leaf);
-            if (r.fin && r.fid >= 0 && (r.mode == TM_CLOSEST || r.mode == TM_EMIT) && a.graze &&
-                grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
-                // the render's grazing-hit rule: traced again on the uncull'd binary path
+            // the render's grazing-hit rule, under the render's own conditions: an
+            // extension ray's closest hit (mode 1), a probe's pass-1 emitter hit (mode 3,
+            // TM_EMIT only -- a probe that trav_begin turned into a closest-hit walk
+            // because the scene has no emissive tree is not re-traced by k_trace either)
+            if (r.fin && r.fid >= 0 && ((mode == 1 && r.mode == TM_CLOSEST) || (mode == 3 && r.mode == TM_EMIT)) &&
+                a.graze && grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
+                // traced again on the uncull'd binary path
                 trav_begin(r, ro, rdir, r.mode, a.boxes_finite != 0, a.emit_root, a.cull_eps, true);
                 trav_lane<true>(r, a, stk, c_ovf);
             }
