@@ -281,6 +281,14 @@ tpt_status tpt_debug_trace_rays(tpt_scene* scene, uint32_t n, const float* origi
  *        inv_cos_cone_diff p3)                              out 6 (dir3, radiance3)
  *   op 3 Spectrum::toUChar in 3                             out 3 (bytes as floats) */
 tpt_status tpt_debug_hot_kat(int device, int32_t op, uint32_t n, const float* in, float* out);
+/* Diagnostics: the per-step latency of ONE 64-lane wave walking n <= 64 closest-hit rays
+ * with the render's traversal ("The drained chain"); mode 0 reads the
+ * 4-wide nodes from global memory as the render does, 1 from a copy of the whole main tree
+ * in LDS; flags TPT_FLAG_FAST: the tolerance-mode build.  out: 4 words per lane (64 lanes):
+ * visits + leaf tests of the lane, loop iterations of the wave, shader cycles of the wave's
+ * walk (s_memtime), hit fid. */
+tpt_status tpt_debug_step_latency(tpt_scene* scene, uint32_t n, const float* origins, const float* dirs,
+                                  int32_t mode, int32_t flags, uint64_t* out);
 /* Host-only: the SAH 4-wide traversal tree tpt_scene_build uploads, over n >= 2
  * leaf boxes (6 floats each, by LBVH sorted position) and emitter flags.  Writes
  * at most `cap` nodes of 32 floats (inner4 layout, device_api.hpp) and the

@@ -237,6 +237,17 @@ class DeviceScene:
                                          _ptr(uv)))
         return hit, t, uv
 
+    def step_latency(self, origins, dirs, mode=0, flags=0):
+        """ONE 64-lane wave walks these <= 64 closest-hit rays (tpt_debug_step_latency):
+        mode 0 nodes from global memory, 1 the whole 4-wide tree in LDS.  Returns
+        (steps per lane, wave loop iterations, wave shader cycles, hit fids)."""
+        o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)
+        out = np.zeros((64, 4), np.uint64)
+        check(lib().tpt_debug_step_latency(self.handle, len(o), _ptr(o), _ptr(d), mode, flags, _ptr(out)))
+        n = len(o)
+        return out[:n, 0].astype(np.int64), int(out[0, 1]), int(out[0, 2]), out[:n, 3].astype(np.int64)
+
     def close(self):
         if self.handle:
             lib().tpt_scene_destroy(self.handle)

@@ -103,6 +103,8 @@ SIGNATURES = [
     ("tpt_debug_trace_rays", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                        C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tpt_debug_hot_kat", C.c_int, [C.c_int, C.c_int32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("tpt_debug_step_latency", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32,
+                                         C.c_void_p]),
     ("tpt_wide_tree_build", C.c_int32, [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                         C.POINTER(C.c_int32), C.c_int32]),
     ("tpt_gltf_load", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
@@ -154,7 +156,12 @@ def lib():
             raise ImportError(f"libtpt.so not found at {LIB_PATH}: build it with "
                               f"`make -C {HERE}` or __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)
+        # TPT_LIB (tools/gpu_abn.sh A/B of an older build) may name a library that
+        # predates the newest debug entry points; the product library must export all
+        older = bool(os.environ.get("TPT_LIB"))
         for name, res, args in SIGNATURES:
+            if older and name.startswith("tpt_debug_") and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -236,6 +236,9 @@ hipError_t launch_wavefront(WfArgs w, uint32_t* h_count, hipEvent_t ev[2], int32
 // trace.hip
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
 hipError_t launch_trace_ptr(const void* a, hipStream_t s);   // a: const TraceArgs*
+// lone-wave step latency probe (tpt_debug_step_latency), a: const TraceArgs*
+hipError_t launch_step_latency_ptr(const void* a, uint32_t n, const float* o, const float* d, int nodes_lds,
+                                   unsigned long long* out, hipStream_t s);
 hipError_t launch_resolve(const ResolveArgs& a, hipStream_t s);
 // KAT kernel over the trace kernel's device functions (tpt_debug_hot_kat)
 hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipStream_t s);
@@ -248,4 +251,6 @@ hipError_t launch_trace_rays(const TraceArgs& a, uint32_t n, const float* o, con
 // the same kernels in namespace tpt_fast, reached with a tpt::TraceArgs.
 namespace tpt_fast {
 hipError_t launch_trace_ptr(const void* a, hipStream_t s);
+hipError_t launch_step_latency_ptr(const void* a, uint32_t n, const float* o, const float* d, int nodes_lds,
+                                   unsigned long long* out, hipStream_t s);
 }

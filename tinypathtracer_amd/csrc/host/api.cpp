@@ -1638,6 +1638,39 @@ tpt_status tpt_debug_trace_rays(tpt_scene* s, uint32_t n, const float* o, const 
     return TPT_OK;
 }
 
+tpt_status tpt_debug_step_latency(tpt_scene* s, uint32_t n, const float* o, const float* d, int32_t mode,
+                                  int32_t flags, uint64_t* out) {
+    if (!s || !s->built) return fail(TPT_ERR_INVALID_ARG, "scene not built");
+    if (n > 64 || (n && (!o || !d || !out))) return fail(TPT_ERR_INVALID_ARG, "1..64 rays and outputs");
+    if (mode < 0 || mode > 1) return fail(TPT_ERR_INVALID_ARG, "mode: 0 nodes in global memory, 1 in LDS");
+    {
+        const tpt_status bs = finish_pending(s);
+        if (bs != TPT_OK) return bs;
+    }
+    const int nodes_lds = mode == 1 ? s->n4 : 0;
+    if ((size_t)nodes_lds * 128 + 64 * 64 * sizeof(int) > 160 * 1024)
+        return fail(TPT_ERR_INVALID_ARG, "the 4-wide tree does not fit in LDS");
+    DeviceGuard g(s->device);
+    DevBuf<float> dorg, ddir;
+    DevBuf<unsigned long long> dout;
+    HIP_OR_FAIL(dorg.upload(o, 3 * (size_t)std::max(n, 1u), s->stream));
+    HIP_OR_FAIL(ddir.upload(d, 3 * (size_t)std::max(n, 1u), s->stream));
+    HIP_OR_FAIL(dout.alloc(4 * 64));
+    tpt::TraceArgs a{};
+    fill_trace_args(s, nullptr, nullptr, a);
+    if (flags & TPT_FLAG_FAST) {   // the tolerance-mode build, without the culling guards
+        a.cull_eps = 0.0f;
+        a.n_sliver_groups = 0;
+        a.graze = 0;
+        HIP_OR_FAIL(tpt_fast::launch_step_latency_ptr(&a, n, dorg.p, ddir.p, nodes_lds, dout.p, s->stream));
+    } else {
+        HIP_OR_FAIL(tpt::launch_step_latency_ptr(&a, n, dorg.p, ddir.p, nodes_lds, dout.p, s->stream));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(s->stream));
+    HIP_OR_FAIL(hipMemcpy(out, dout.p, 4 * 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return TPT_OK;
+}
+
 tpt_status tpt_debug_hot_kat(int device, int32_t op, uint32_t n, const float* in, float* out) {
     static const int kIn[4] = {12, 15, 16, 3}, kOut[4] = {2, 4, 6, 3};
     if (op < 0 || op > 3) return fail(TPT_ERR_INVALID_ARG, "unknown KAT op");

@@ -1257,6 +1257,91 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Lone-wave step latency (tpt_debug_step_latency; DESIGN.md section 6, "The
+// drained chain"): ONE 64-lane wave walks up to 64 rays with the production
+// closest-hit traversal (4-wide ordered visits, leaves tested when reached, as
+// k_trace_rays mode 1 minus the sliver pass), its 4-wide nodes read from global
+// memory (nodes_lds 0, what k_trace does) or from a copy of the first
+// nodes_lds nodes in LDS (the whole main tree: every visit an LDS read), the
+// stack in LDS either way.  out[4 * lane]: this lane's visits + leaf tests,
+// the wave's loop iterations, the wave's shader cycles (s_memtime) for the
+// walk, the hit fid.
+constexpr int kLatStackSlots = 64;
+__global__ __launch_bounds__(64) void k_step_latency(TraceArgs a, uint32_t n, const float* __restrict__ o,
+                                                     const float* __restrict__ d, int nodes_lds,
+                                                     unsigned long long* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    TPT_LDS char* slds = (TPT_LDS char*)lds;
+    const int lane = threadIdx.x;
+    TPT_LDS LdsF4* snodes = (TPT_LDS LdsF4*)slds;
+    for (int i = lane; i < 8 * nodes_lds; i += 64) {
+        const float4 m = a.inner4[i];
+        snodes[i].x = m.x;
+        snodes[i].y = m.y;
+        snodes[i].z = m.z;
+        snodes[i].w = m.w;
+    }
+    __syncthreads();
+    LaneStack<int> stk;
+    stk.lds = (TPT_LDS int*)(slds + (size_t)nodes_lds * 128) + lane;
+    stk.nlds = kLatStackSlots;
+    const int nint = a.n_faces - 1;
+    const bool active = (uint32_t)lane < n;
+    Trav r;
+    trav_begin(r, active ? v3(o[3 * lane], o[3 * lane + 1], o[3 * lane + 2]) : v3(0.0f, 0.0f, 0.0f),
+               active ? v3(d[3 * lane], d[3 * lane + 1], d[3 * lane + 2]) : v3(1.0f, 1.0f, 1.0f), TM_CLOSEST,
+               a.boxes_finite != 0, a.emit_root, a.cull_eps, false);
+    if (!active) r.node = -1;
+    unsigned long long steps = 0, iters = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    while (__ballot(r.node >= 0) != 0ull) {
+        ++iters;
+        if (r.node >= 0) {
+            ++steps;
+            if (r.node < nint) {
+                int next;
+                if (r.fin) {
+                    if (r.node < nodes_lds) {
+                        const TPT_LDS LdsF4* nd = snodes + 8 * r.node;
+                        next = inner_visit4_q(r, lds_f4(nd), lds_f4(nd + 1), lds_f4(nd + 2), lds_f4(nd + 3),
+                                              lds_f4(nd + 4), lds_f4(nd + 5), lds_f4(nd + 6), stk, r.sp);
+                    } else {
+                        next = inner_visit4(r, a.inner4, nullptr, 0, stk, r.sp);
+                    }
+                } else {
+                    int deferred;
+                    bool push;
+                    inner_visit<true>(r, a.inner, next, push, deferred);
+                    stk.put(r.sp, deferred);
+                    r.sp += push ? 1 : 0;
+                }
+                if (r.sp > a.stack_depth) {
+                    r.sp = 0;
+                    next = -1;
+                }
+                r.node = next >= 0 ? next : (r.sp == 0 ? -1 : stk.get(--r.sp));
+            } else {
+                const bool stop = leaf_test<true>(r, a.tri, r.node - nint, a.cull_eps);
+                r.node = (stop || r.sp == 0) ? -1 : stk.get(--r.sp);
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[4 * lane] = steps;
+    out[4 * lane + 1] = iters;
+    out[4 * lane + 2] = t1 - t0;
+    out[4 * lane + 3] = (unsigned long long)(long long)r.fid;
+}
+hipError_t launch_step_latency_ptr(const void* a, uint32_t n, const float* o, const float* d, int nodes_lds,
+                                   unsigned long long* out, hipStream_t s) {
+    const size_t lds = (size_t)nodes_lds * 128 + (size_t)kLatStackSlots * 64 * sizeof(int);
+    hipLaunchKernelGGL(k_step_latency, dim3(1), dim3(64), lds, s, *static_cast<const TraceArgs*>(a), n, o, d,
+                       nodes_lds, out);
+    return hipGetLastError();
+}
+
 // The host calls the tolerance-mode build (namespace tpt_fast, the same TraceArgs
 // layout) through this entry point.
 hipError_t launch_trace_ptr(const void* a, hipStream_t s) { return launch_trace(*static_cast<const TraceArgs*>(a), s); }

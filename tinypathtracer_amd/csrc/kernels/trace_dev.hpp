@@ -360,6 +360,9 @@ __device__ __forceinline__ float4 lds_f4(const TPT_LDS LdsF4* p) { return make_f
 // constraints outweigh the halved instruction count)
 
 template <typename StackT>
+__device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q1, float4 q2, float4 q3, float4 q4,
+                                              float4 q5, float4 q6, LaneStack<StackT>& stk, int& sp);
+template <typename StackT>
 __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4,
                                             const TPT_LDS LdsF4* snodes, int nlds_nodes, LaneStack<StackT>& stk,
                                             int& sp) {
@@ -383,6 +386,12 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
         q5 = nd[5];
         q6 = nd[6];
     }
+    return inner_visit4_q(r, q0, q1, q2, q3, q4, q5, q6, stk, sp);
+}
+// the visit's arithmetic on the node's seven float4 (from global memory or LDS)
+template <typename StackT>
+__device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q1, float4 q2, float4 q3, float4 q4,
+                                              float4 q5, float4 q6, LaneStack<StackT>& stk, int& sp) {
     float k0, k1, k2, k3, e0, e1, e2, e3;
     slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
