@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 TAG=${1:-r02}; NAME=${2:-c2}; shift 2
 ARGS="$@"
 mkdir -p gpurun_out
-bash tools/profile.sh ${TAG}_$NAME --steps 1 --warmup 0 --cpu-baseline 0 $ARGS > gpurun_out/profile_${TAG}_$NAME.log 2>&1 || { echo PROFILE FAILED; tail -5 gpurun_out/profile_${TAG}_$NAME.log; exit 1; }
+bash tools/profile.sh ${TAG}_$NAME --steps 1 --warmup 0 --cpu-baseline 0 --fast-extra 0 $ARGS > gpurun_out/profile_${TAG}_$NAME.log 2>&1 || { echo PROFILE FAILED; tail -5 gpurun_out/profile_${TAG}_$NAME.log; exit 1; }
 mkdir -p gpurun_out/stage_profiles && cp gpurun_out/prof_${TAG}_$NAME/summary.json gpurun_out/stage_profiles/${TAG}_pmc_summary_$NAME.json
 f=$(ls gpurun_out/prof_${TAG}_$NAME/ktrace/*/*kernel_stats.csv gpurun_out/prof_${TAG}_$NAME/ktrace/*kernel_stats.csv 2>/dev/null | head -1)
 [ -n "$f" ] && cp "$f" gpurun_out/stage_profiles/${TAG}_kernel_stats_$NAME.csv
