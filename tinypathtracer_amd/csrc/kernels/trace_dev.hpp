@@ -23,6 +23,12 @@
 // 8(d)'s per-channel tolerance, not bit for bit.
 #define TPT_FAST 0
 #endif
+#ifndef TPT_FAST_SINCOS   // tolerance build: hardware v_sin/v_cos in the hemisphere sampler (0: the parity sincos)
+#define TPT_FAST_SINCOS 1
+#endif
+#ifndef TPT_FAST_RCP      // tolerance build: v_rcp_f32 for 1/d and the triangle test's 1/denom (0: IEEE divides)
+#define TPT_FAST_RCP 1
+#endif
 #ifndef TPT_PROBE_SHORTCUT
 #define TPT_PROBE_SHORTCUT 1   // no emissive triangle: resolve direct probes in the shading pass
 #endif
@@ -209,7 +215,7 @@ __device__ __forceinline__ void trav_begin(Trav& r, V3 o, V3 d, int mode, bool b
                                            int emit_root = -1, float cull_eps = 0.0f, bool graze = false) {
     r.o = o;
     r.d = d;
-    if (TPT_FAST)
+    if (TPT_FAST && TPT_FAST_RCP)
         r.inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     else
         r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);   // rayHitBBox :20, hoisted
@@ -461,7 +467,7 @@ __device__ __forceinline__ bool tri_core(const V3& o, const V3& d, const V3& v0,
     const V3 p = cross(d, e2);
     const V3 q = cross(tv, e1);
     const float denom = dot(p, e1);
-    const float id = TPT_FAST ? __builtin_amdgcn_rcpf(denom) : 1.0f / denom;
+    const float id = (TPT_FAST && TPT_FAST_RCP) ? __builtin_amdgcn_rcpf(denom) : 1.0f / denom;
     u = dot(p, tv) * id;
     v = dot(q, d) * id;
     t = dot(q, e2) * id;
@@ -744,7 +750,7 @@ __device__ __forceinline__ float new_direction(V3 d, V3 n, float eta_m, float me
     // HemisphereCosine (sampler.h:75-89)
     const V3 zb = cross(xb, n);
     float sp, cp;
-#if TPT_FAST
+#if TPT_FAST && TPT_FAST_SINCOS
     // v_sin_f32 / v_cos_f32 take revolutions: sin(2 pi u) directly
     const float u_phi = xorwow_uniform(st);
     const float cos_t = __builtin_amdgcn_sqrtf(xorwow_uniform(st));
