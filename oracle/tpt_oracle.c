@@ -738,7 +738,12 @@ static int env_is_sample(const orc_env* env, const env_is_t* t, v3 nf, uint32_t 
     const float pb = ((hi2 - lo2) / rs) * ((hi1 - lo1) / t->total);
     const float pdf = (pb * (((float)W * (float)H) / (float)(wb * hb))) / ((2.0f * PI_F * PI_F) * sth);
     if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < 3.40282347e+38f)) return 0;
-    const v3 le = env_lookup(env, *dir, tm);
+    /* Le: the texel the sample lies in (the lookup of dir up to rounding at texel edges) */
+    (void)tm;
+    const int fx = (int)(f2 * (float)wb), fy = (int)(f1 * (float)hb);
+    const int ix = x0 + (fx < wb - 1 ? fx : wb - 1), iy = y0 + (fy < hb - 1 ? fy : hb - 1);
+    const uint8_t* px = env->rgba + 4 * ((size_t)iy * (size_t)W + (size_t)ix);
+    const v3 le = vscale(1.0f / 255.0f, V3((float)px[0], (float)px[1], (float)px[2]));
     const float k = c / (PI_F * pdf);
     *k_le = vscale(k, le);
     return 1;

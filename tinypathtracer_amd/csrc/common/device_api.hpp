@@ -17,7 +17,7 @@
 //     (non-finite boxes, or a tree deeper than the stack): the LBVH's
 //     even-depth nodes, each holding its up to 4 grandchildren (a leaf child
 //     stands for itself), bit 30 = emitter (ignored).
-//   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0)
+//   tri[3*F] float4    leaf slot j: (v0.xyz, bits(fid)), (e1.xyz, 0), (e2.xyz, 0) (tri_rec.hpp)
 //   shade[3*F] float4  face fid: (n0.xyz, bits(mtl)), (n1.xyz, geometric unit normal .x, sign of .z in
 //                      its lowest bit; NaN: none), (n2.xyz, geometric normal .y)
 //   mtl[2*M] float4    (base.rgb, emission), (eta, metallic, 0, 0)

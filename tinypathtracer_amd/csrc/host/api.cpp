@@ -24,6 +24,7 @@
 #include "../common/ptrig.hpp"
 #include "../common/rng.hpp"
 #include "../common/tpt_math.hpp"
+#include "../common/tri_rec.hpp"
 #include "tpt.h"
 #include "tpt_internal.hpp"
 
@@ -738,7 +739,7 @@ static tpt_status scene_build(tpt_scene* s, bool async) {
     HIP_OR_FAIL(s->sort_tmp.alloc(std::max<size_t>(sort_bytes, 16)));
     HIP_OR_FAIL(s->inner.alloc(4 * std::max<size_t>(n - 1, 1)));
     HIP_OR_FAIL(s->inner4.alloc(8 * std::max<size_t>(n - 1, 1)));
-    HIP_OR_FAIL(s->tri.alloc(3 * n));
+    HIP_OR_FAIL(s->tri.alloc(tpt::tri_float4s(n)));
     HIP_OR_FAIL(s->shade.alloc(3 * n));
     HIP_OR_FAIL(s->nodes36.alloc(36 * nn));
     HIP_OR_FAIL(hipMemsetAsync(s->parent.p, 0, nn * sizeof(uint32_t), s->stream));

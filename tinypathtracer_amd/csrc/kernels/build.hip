@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../common/device_api.hpp"
+#include "../common/tri_rec.hpp"
 #include "../common/tpt_math.hpp"
 
 namespace tpt {
@@ -278,10 +279,7 @@ __global__ void k_pack_leaf(BuildBuffers b) {
     const V3 p1 = v3(w[3 * i1], w[3 * i1 + 1], w[3 * i1 + 2]);
     const V3 p2 = v3(w[3 * i2], w[3 * i2 + 1], w[3 * i2 + 2]);
     const V3 e1 = p1 - p0, e2 = p2 - p0;   // rayHitTriangle :66-67, hoisted (same rounding)
-    float4* t = b.tri + 3 * j;
-    t[0] = make_float4(p0.x, p0.y, p0.z, __int_as_float((int)fid));
-    t[1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
-    t[2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+    tri_store(b.tri, j, p0.x, p0.y, p0.z, (int)fid, e1.x, e1.y, e1.z, e2.x, e2.y, e2.z);
 }
 
 __global__ void k_pack_shade(BuildBuffers b) {
@@ -343,7 +341,8 @@ __global__ __launch_bounds__(256) void k_sliver_scan(const float4* __restrict__ 
     const int p = blockIdx.x * 256 + threadIdx.x;
     double m = 0.0;
     if (p < n) {
-        const float4 q0 = tri[3 * p], q1 = tri[3 * p + 1], q2 = tri[3 * p + 2];
+        const TriQ tq = tri_load(tri, p);
+        const float4 q0 = tq.q0, q1 = tq.q1, q2 = tq.q2;
         const double a0 = q1.x, a1 = q1.y, a2 = q1.z, b0 = q2.x, b1 = q2.y, b2 = q2.z;
         const double c0 = a1 * b2 - a2 * b1, c1 = a2 * b0 - a0 * b2, c2 = a0 * b1 - a1 * b0;
         const double la = sqrt(a0 * a0 + a1 * a1 + a2 * a2);

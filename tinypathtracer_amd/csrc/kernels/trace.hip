@@ -800,10 +800,10 @@ void k_trace(TraceArgs a) {
                     r.pend = r.node - nint;
                     r.node = r.sp == 0 ? -1 : stk.get(--r.sp);
                     if constexpr (DRAIN) {
-                        const float4* tr = a.tri + 3 * r.pend;   // in flight while the walk goes on
-                        pq0 = tr[0];
-                        pq1 = tr[1];
-                        pq2 = tr[2];
+                        const TriQ tq = tri_load(a.tri, r.pend);   // in flight while the walk goes on
+                        pq0 = tq.q0;
+                        pq1 = tq.q1;
+                        pq2 = tq.q2;
                     }
                 }
                 has = r.pend >= 0;
@@ -1168,6 +1168,21 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
     return head + stack + levels * level;
 }
 
+// pixel pool (k_trace): two tiles per workgroup, the second drawn from by the
+// lanes that finish their pixel first; its LDS counter follows the rest
+static void use_tile_pool(TraceArgs& a, dim3& grid, size_t& lds) {
+    a.tile_pool = 1;
+    grid.x = (grid.x + 1) / 2;
+    if (a.xcd_run > 0) {   // runs of workgroups now: half as many, each two tiles wide
+        const int per = grid.x % 8 == 0 ? (int)grid.x / 8 : 0, want = std::max(2, a.xcd_run / 2);
+        a.xcd_run = 0;
+        for (int g = std::min(per, want); g >= 2 && a.xcd_run == 0; --g)
+            if (per % g == 0) a.xcd_run = g;
+    }
+    a.lds_pool_offset = (int)((lds + 15) / 16 * 16);
+    lds = (size_t)a.lds_pool_offset + 16;
+}
+
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     TraceArgs a = a_in;
     a.tile_pool = 0;
@@ -1221,22 +1236,10 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    // pixel pool (k_trace): two tiles per workgroup, the second drawn from by the
-    // lanes that finish their pixel first; its LDS counter comes out of the budget
+    // pixel pool; its LDS counter comes out of the budget
     const bool use_pool = TPT_TILE_POOL && !a.drained;
     size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudget - (use_pool ? 16 : 0));
-    if (use_pool) {
-        a.tile_pool = 1;
-        grid.x = (grid.x + 1) / 2;
-        if (a.xcd_run > 0) {   // runs of workgroups now: half as many, each two tiles wide
-            const int per = grid.x % 8 == 0 ? (int)grid.x / 8 : 0, want = std::max(2, a.xcd_run / 2);
-            a.xcd_run = 0;
-            for (int g = std::min(per, want); g >= 2 && a.xcd_run == 0; --g)
-                if (per % g == 0) a.xcd_run = g;
-        }
-        a.lds_pool_offset = (int)((lds + 15) / 16 * 16);
-        lds = (size_t)a.lds_pool_offset + 16;
-    }
+    if (use_pool) use_tile_pool(a, grid, lds);
     if (lights) {
         if (mtl_lds) {
             if (small) launch_ordered<true, true, uint16_t>(a, grid, lds, s);

@@ -12,6 +12,7 @@
 #include "../common/device_api.hpp"
 #include "../common/ptrig.hpp"
 #include "../common/rng.hpp"
+#include "../common/tri_rec.hpp"
 #include "../common/tpt_math.hpp"
 #include "tpt.h"
 
@@ -497,8 +498,8 @@ __device__ __forceinline__ bool leaf_test_q(Trav& r, const float4 q0, const floa
 }
 template <bool ORDERED>
 __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos, float cull_eps) {
-    const float4* tr = tri + 3 * pos;
-    return leaf_test_q<ORDERED>(r, tr[0], tr[1], tr[2], pos, cull_eps);
+    const TriQ tq = tri_load(tri, pos);
+    return leaf_test_q<ORDERED>(r, tq.q0, tq.q1, tq.q2, pos, cull_eps);
 }
 
 // Probe pass 1 over an emissive-triangle tree that is a single 4-wide node of
@@ -527,18 +528,21 @@ __device__ __forceinline__ void emit_probe_inline(Trav& r, const float4* __restr
         if (i3 >= 0) slab_minmax(r.o, r.inv, q4.z, q4.w, q5.x, q5.y, q5.z, q5.w, k3, e3);
         const int p0 = i0 >= 0 ? (i0 & kLinkMask) - nint : 0, p1 = i1 >= 0 ? (i1 & kLinkMask) - nint : 0,
                   p2 = i2 >= 0 ? (i2 & kLinkMask) - nint : 0, p3 = i3 >= 0 ? (i3 & kLinkMask) - nint : 0;
-        const float4 a0 = tri[3 * p0], a1 = tri[3 * p0 + 1], a2 = tri[3 * p0 + 2];
-        const float4 b0 = tri[3 * p1], b1 = tri[3 * p1 + 1], b2 = tri[3 * p1 + 2];
+        const TriQ ta = tri_load(tri, p0), tb = tri_load(tri, p1);
+        const float4 a0 = ta.q0, a1 = ta.q1, a2 = ta.q2;
+        const float4 b0 = tb.q0, b1 = tb.q1, b2 = tb.q2;
         float4 c0 = a0, c1 = a1, c2 = a2, d0 = a0, d1 = a1, d2 = a2;
         if (i2 >= 0) {
-            c0 = tri[3 * p2];
-            c1 = tri[3 * p2 + 1];
-            c2 = tri[3 * p2 + 2];
+            const TriQ tc = tri_load(tri, p2);
+            c0 = tc.q0;
+            c1 = tc.q1;
+            c2 = tc.q2;
         }
         if (i3 >= 0) {
-            d0 = tri[3 * p3];
-            d1 = tri[3 * p3 + 1];
-            d2 = tri[3 * p3 + 2];
+            const TriQ td = tri_load(tri, p3);
+            d0 = td.q0;
+            d1 = td.q1;
+            d2 = td.q2;
         }
         if ((i0 >= 0) & (fmaxf(k0, hd) <= fminf(e0, hi))) { ++c_leaf; leaf_test_q<true>(r, a0, a1, a2, p0, cull_eps); }
         if ((i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi))) { ++c_leaf; leaf_test_q<true>(r, b0, b1, b2, p1, cull_eps); }
@@ -919,7 +923,13 @@ __device__ __forceinline__ bool env_is_sample(const TraceArgs& a, V3 nf, float x
     const float pb = ((hi2 - lo2) / rs) * ((hi1 - lo1) / a.is_total);
     const float pdf = (pb * (((float)W * (float)H) / (float)(wb * hb))) / ((2.0f * kPi * kPi) * sth);
     if (!(sth > 0.0f) || !(c > 0.0f) || !(pdf > 0.0f) || !(pdf < kRealMax)) return false;
-    const V3 le = env_lookup<true>(a.env, W, H, dir);
+    // Le: the texel the sample lies in, (x0 + f2 * wb, y0 + f1 * hb) -- the texel the
+    // lookup of dir (Vec2UV, env_light.cuh:72-78) finds, which inverts the same angles,
+    // up to rounding at texel edges -- read without the atan2 / acos of the lookup
+    const int ix = x0 + min((int)(f2 * (float)wb), wb - 1);
+    const int iy = y0 + min((int)(f1 * (float)hb), hb - 1);
+    const uint32_t tx = a.env[(size_t)iy * (size_t)W + (size_t)ix];
+    const V3 le = (1.0f / 255.0f) * v3((float)(tx & 0xffu), (float)((tx >> 8) & 0xffu), (float)((tx >> 16) & 0xffu));
     const float k = c / (kPi * pdf);
     k_le = k * le;
     return true;
