@@ -111,7 +111,8 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=16)
     ap.add_argument("--spp-per-launch", type=int, default=0)
     ap.add_argument("--lanes-per-pixel", type=int, default=0,
-                    help="tpt_params.lanes_per_pixel: 0 auto, 1, 2 = pair mode (delta-light scenes)")
+                    help="tpt_params.lanes_per_pixel: 0 auto, 1, 2 = pair mode (delta-light scenes), "
+                         "4 = four lanes per pixel (split node visits)")
     ap.add_argument("--pipe-sets", type=int, default=0,
                     help="launch pipeline band sets (tpt_params.pipe_sets): 0 auto, 1 one launch per frame")
     ap.add_argument("--pipe-chunks", type=int, default=0,

@@ -120,8 +120,11 @@ typedef struct {
     int32_t pipe_sets, pipe_chunks;
     /* Lanes per pixel: 0 = auto, 1, or 2 = pair mode (scenes with delta lights): a side
      * lane per pixel traces each bounce's shadow rays while the path lane goes on, so a
-     * sample's serial chain pays one traversal per bounce.
-     * Bit-identical either way. */
+     * sample's serial chain pays one traversal per bounce; 4 = four
+     * lanes run each pixel's path together and split every 4-wide node visit (child k on
+     * lane k, leaf children tested at once), a shorter serial chain at a quarter of the
+     * pixels per wave (scenes without delta lights, no env IS, ordered traversal; DESIGN.md
+     * section 6).  Bit-identical in every mode. */
     int32_t lanes_per_pixel;
     /* 0 = auto: a wave runs its parked triangle tests once this many lanes are blocked on
      * a parked leaf (speculative leaf postponement): 2 in pair mode,
@@ -284,9 +287,11 @@ tpt_status tpt_debug_hot_kat(int device, int32_t op, uint32_t n, const float* in
 /* Diagnostics: the per-step latency of ONE 64-lane wave walking n <= 64 closest-hit rays
  * with the render's traversal ("The drained chain"); mode 0 reads the
  * 4-wide nodes from global memory as the render does, 1 from a copy of the whole main tree
- * in LDS; flags TPT_FLAG_FAST: the tolerance-mode build.  out: 4 words per lane (64 lanes):
- * visits + leaf tests of the lane, loop iterations of the wave, shader cycles of the wave's
- * walk (s_memtime), hit fid. */
+ * in LDS, 2 four lanes per ray (n <= 16: lane k of a ray's quad tests child k of each node,
+ * its leaf children at once; node visits in out's first word); flags TPT_FLAG_FAST: the
+ * tolerance-mode build.  out: 4 words per lane (64 lanes; per ray in mode 2): visits + leaf
+ * tests of the lane, loop iterations of the wave, shader cycles of the wave's walk
+ * (s_memtime), hit fid. */
 tpt_status tpt_debug_step_latency(tpt_scene* scene, uint32_t n, const float* origins, const float* dirs,
                                   int32_t mode, int32_t flags, uint64_t* out);
 /* Host-only: the SAH 4-wide traversal tree tpt_scene_build uploads, over n >= 2

@@ -239,7 +239,8 @@ class DeviceScene:
 
     def step_latency(self, origins, dirs, mode=0, flags=0):
         """ONE 64-lane wave walks these <= 64 closest-hit rays (tpt_debug_step_latency):
-        mode 0 nodes from global memory, 1 the whole 4-wide tree in LDS.  Returns
+        mode 0 nodes from global memory, 1 the whole 4-wide tree in LDS, 2 four lanes
+        per ray (<= 16 rays; steps = node visits, leaf children tested in-node).  Returns
         (steps per lane, wave loop iterations, wave shader cycles, hit fids)."""
         o = np.ascontiguousarray(origins, np.float32).reshape(-1, 3)
         d = np.ascontiguousarray(dirs, np.float32).reshape(-1, 3)

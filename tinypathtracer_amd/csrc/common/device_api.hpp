@@ -105,6 +105,11 @@ struct TraceArgs {
     int32_t graze;                       // 1: rays leaving a face within 1e-3 of its plane skip the culls (grazing())
     int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
     int32_t drained;                     // 1: the launch cannot fill the chip (latency-oriented DRAIN variants)
+    int32_t quad;                        // 1: four lanes per pixel, each node visit split over them (k_trace QUAD)
+    const int32_t* tile_list;            // non-null: workgroup b renders tile tile_list[b] = row block << 16 | column
+                                         //    (16x16 tiles, QUAD 8x8; one frame; no pixel pool)
+    int32_t n_tiles;                     // entries of tile_list (the grid)
+    uint32_t* pix_cost;                  // non-null: each pixel's rays in this launch (one lane per pixel, no pool)
     int32_t xcd_run;                     // > 0: workgroup tiles dealt to XCDs in runs of this many (k_trace)
     int32_t tile_pool;                   // 1: each workgroup renders two adjacent tiles, the second as a pixel
                                          //    pool its finished lanes draw from (k_trace; set by launch_trace)
@@ -235,6 +240,7 @@ hipError_t launch_wavefront(WfArgs w, uint32_t* h_count, hipEvent_t ev[2], int32
 
 // trace.hip
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
+bool trace_quad_fits(const TraceArgs& a);   // lanes_per_pixel 4: one-lane records, the quads' stacks fit in LDS
 hipError_t launch_trace_ptr(const void* a, hipStream_t s);   // a: const TraceArgs*
 // lone-wave step latency probe (tpt_debug_step_latency), a: const TraceArgs*
 hipError_t launch_step_latency_ptr(const void* a, uint32_t n, const float* o, const float* d, int nodes_lds,

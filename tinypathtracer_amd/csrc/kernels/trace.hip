@@ -99,11 +99,14 @@ __device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int p
 // bit-identical.  A pixel's sample chain then pays one traversal per bounce
 // instead of 1 + lights, which is what bounds tail-heavy frames (C3).
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
-          bool PAIR = false, bool DRAIN = false>
+          bool PAIR = false, bool DRAIN = false, bool QUAD = false>
 __global__ __launch_bounds__(256, ENVIS ? TPT_TRACE_WAVES_IS
-                                        : (PAIR ? TPT_TRACE_WAVES_PAIR : (DRAIN ? TPT_TRACE_WAVES_DRAIN : TPT_TRACE_WAVES)))
+                                        : (PAIR ? TPT_TRACE_WAVES_PAIR
+                                                : (QUAD ? TPT_TRACE_WAVES_QUAD
+                                                        : (DRAIN ? TPT_TRACE_WAVES_DRAIN : TPT_TRACE_WAVES))))
 void k_trace(TraceArgs a) {
     static_assert(!PAIR || (ORDERED && LIGHTS), "pair mode: ordered variants with 5-word records");
+    static_assert(!QUAD || (ORDERED && !LIGHTS && !PAIR && !ENVIS && !DRAIN), "four lanes per pixel: one-lane logic");
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     // grid y interleaves the frames of a batch: consecutive workgroups render the
@@ -111,6 +114,11 @@ void k_trace(TraceArgs a) {
     // screen locality of a single frame (node reuse in L1/L2)
     const int nfr = a.n_frames > 0 ? a.n_frames : 1;
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    if (a.tile_list) {   // a listed subset of the tiles (host render_hybrid; one frame)
+        const int t = a.tile_list[blockIdx.x];
+        bx = t & 0xffff;
+        by = t >> 16;
+    }
     // XCD runs (scenes larger than an XCD's 4 MiB L2): blocks b and b + 8 share
     // an XCD.  Within each row of workgroups XCD k gets runs of xcd_run
     // adjacent tiles instead of every 8th tile, so its resident tiles see less
@@ -135,9 +143,14 @@ void k_trace(TraceArgs a) {
     const int tx = pool ? 2 * bx : bx;
     // pair mode: lane 2q (path) and 2q + 1 (side) serve pixel q of the wave's 8x4 tile
     const bool side = PAIR && (lane & 1);
-    const int pl = PAIR ? (lane >> 1) : lane;   // pixel slot in the wave
-    int x = tx * 16 + (wave & 1) * 8 + (pl & 7);
-    const int ly = PAIR ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3) : (by / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
+    // QUAD: lanes 4q..4q+3 all run pixel q of the wave's 4x4 tile (8x8 pixels per
+    // workgroup) with the same state; lane 4q (lead) counts and stores it
+    const bool lead = !QUAD || (lane & 3) == 0;
+    const int pl = PAIR ? (lane >> 1) : (QUAD ? (lane >> 2) : lane);   // pixel slot in the wave
+    int x = QUAD ? tx * 8 + (wave & 1) * 4 + (pl & 3) : tx * 16 + (wave & 1) * 8 + (pl & 7);
+    const int ly = PAIR   ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3)
+                   : QUAD ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 2)
+                          : (by / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
     int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
     const bool pixel = x < a.width && ly < a.band_height && y < a.height;
     bool active = pixel && !side;   // owns the pixel's RNG stream and sums
@@ -183,8 +196,10 @@ void k_trace(TraceArgs a) {
             return a.mtl[i];
         }
     };
-    LaneStack<StackT> stk;
-    stk.lds = (TPT_LDS StackT*)(slds + a.lds_stack_offset) + ((TPT_STACK_PAIRED && sizeof(StackT) == 2) ? 2 * tid : tid);
+    // (QUAD: one stack per quad in its four lanes' columns; the host keeps it all in LDS)
+    LaneStack<StackT, QUAD> stk;
+    stk.lds = (TPT_LDS StackT*)(slds + a.lds_stack_offset) +
+              ((TPT_STACK_PAIRED && sizeof(StackT) == 2) ? 2 * tid : (QUAD ? (tid & ~3) : tid));
     stk.nlds = a.stack_lds_slots;
     PathRecords<MAXD, PAIR ? 128 : 256> rec;
     rec.lds = (TPT_LDS float*)(slds + a.lds_rec_offset) + (PAIR ? wave * 32 + pl : tid);
@@ -757,14 +772,14 @@ void k_trace(TraceArgs a) {
 #ifdef TPT_PROFILE_PHASES
             ++p_steps;
 #endif
-            const int cnt = __popcll(__ballot(ts == TS_TRAV));
+            const int cnt = __popcll(__ballot(lead && ts == TS_TRAV));   // (QUAD: pixels)
 #ifdef TPT_PROFILE_PHASES
             p_lt += (unsigned long long)cnt;
             p_lw += (unsigned long long)__popcll(__ballot(ts == TS_DONE));
             p_lx += (unsigned long long)__popcll(__ballot(ts == TS_DEAD || ts == TS_IDLE));
 #endif
             if (cnt == 0) break;
-            if (cnt < thr && __ballot(ts == TS_DONE) != 0ull) break;
+            if (cnt < thr && __ballot(lead && ts == TS_DONE) != 0ull) break;
             // Speculative leaf postponement: a lane that reaches a leaf parks it
             // (one slot) and keeps walking inner nodes; the wave runs the
             // triangle branch only when enough lanes hold a parked leaf, when
@@ -778,7 +793,15 @@ void k_trace(TraceArgs a) {
             if (ts == TS_TRAV) {
                 if (at_inner) {
                     int next;
-                    if (ORDERED && r.fin) {   // 4-wide (r.fin includes a.boxes_finite)
+                    if (QUAD && r.fin) {   // 4-wide, split over the pixel's four lanes
+                        ++c_wide;
+                        bool stop;
+                        next = inner_visit4_quad(r, a.inner4, a.tri, nint, a.cull_eps, stk, r.sp, stop, c_leaf);
+                        if (stop) {
+                            r.sp = 0;
+                            next = -1;
+                        }
+                    } else if (ORDERED && r.fin) {   // 4-wide (r.fin includes a.boxes_finite)
                         ++c_wide;
                         next = inner_visit4(r, a.inner4, snodes, a.lds_nodes, stk, r.sp);
                     } else {                  // binary, the reference's exact slab test
@@ -828,12 +851,16 @@ void k_trace(TraceArgs a) {
             if (ts == TS_TRAV && r.node < 0 && r.pend < 0) ts = TS_DONE;
         }
     }
-    if (active) {
+    if (active && lead) {
 #pragma unroll
         for (int i = 0; i < 6; ++i) g_rng[i * npix + off] = st[i];
         g_acc[off] = total.x;
         g_acc[npix + off] = total.y;
         g_acc[2 * npix + off] = total.z;
+    }
+    if (a.pix_cost && pixel && lead) a.pix_cost[off] = c_trav;   // (one lane per pixel, no pool)
+    if (!lead) {   // QUAD: the pixel's work is counted once
+        c_trav = c_inner = c_wide = c_leaf = c_shade = c_ovf = c_local = 0;
     }
     const unsigned long long s_wide = wave_sum(c_wide), s_local = wave_sum(c_local);
     const unsigned long long s_trav = wave_sum(c_trav), s_inner = wave_sum(c_inner), s_leaf = wave_sum(c_leaf),
@@ -1083,10 +1110,21 @@ hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipSt
 }
 
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
-          bool PAIR = false, bool DRAIN = false>
+          bool PAIR = false, bool DRAIN = false, bool QUAD = false>
 static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR, DRAIN>), grid, dim3(256), lds,
-                       s, a);
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR, DRAIN, QUAD>), grid,
+                       dim3(256), lds, s, a);
+}
+// four lanes per pixel (a.quad): one-lane logic without delta lights
+template <bool MTL_LDS, typename StackT>
+static void launch_quad(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if (TPT_PROBE_INLINE && a.emit_inline) {
+        if (a.max_depth <= 8) launch_one<8, true, false, MTL_LDS, StackT, false, true, false, false, true>(a, grid, lds, s);
+        else launch_one<64, true, false, MTL_LDS, StackT, false, true, false, false, true>(a, grid, lds, s);
+    } else {
+        if (a.max_depth <= 8) launch_one<8, true, false, MTL_LDS, StackT, false, false, false, false, true>(a, grid, lds, s);
+        else launch_one<64, true, false, MTL_LDS, StackT, false, false, false, false, true>(a, grid, lds, s);
+    }
 }
 
 // INL: probe pass 1 in the shading pass (an emissive tree of one node); its own
@@ -1120,6 +1158,7 @@ static void launch_ordered(const TraceArgs& a, dim3 grid, size_t lds, hipStream_
 constexpr size_t kLdsBudget = (163840 / TPT_TRACE_WAVES) & ~(size_t)255;
 constexpr size_t kLdsBudgetIS = (163840 / TPT_TRACE_WAVES_IS) & ~(size_t)255;
 constexpr size_t kLdsBudgetPair = (163840 / TPT_TRACE_WAVES_PAIR) & ~(size_t)255;
+constexpr size_t kLdsBudgetQuad = (163840 / TPT_TRACE_WAVES_QUAD) & ~(size_t)255;
 #ifndef TPT_MTL_LDS_MAX
 #define TPT_MTL_LDS_MAX 2048
 #endif
@@ -1127,7 +1166,7 @@ constexpr size_t kLdsMtlMax = TPT_MTL_LDS_MAX;   // material tables up to 64 ent
 constexpr size_t kLdsNodesMax = TPT_LDS_NODES_MAX;
 
 size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool wide, int rec_cols = 256,
-                       size_t lds_budget = kLdsBudget) {
+                       size_t lds_budget = kLdsBudget, bool quad = false) {
     // [material table][top 4-wide nodes][traversal stack][path records].
     // Priorities (measured on box): the whole stack (a
     // stack capped at 23 of its 40 slots cost 7 %), then path records up to
@@ -1137,7 +1176,7 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
     a.mtl_in_lds = mtl_lds ? 1 : 0;
     a.lds_mtl_offset = 0;
     const size_t budget = lds_budget - mtl_bytes;
-    const size_t slot = 256 * elem;
+    const size_t slot = quad ? 64 * elem : 256 * elem;   // (quad: four slots per 256-lane row)
     const size_t level = (size_t)words * (size_t)rec_cols * sizeof(float);
     // The whole stack (capacity + 3 spare slots for the unconditional 4-wide
     // pushes) when the path records of max_depth levels fit beside it.  Else
@@ -1153,7 +1192,8 @@ size_t trace_lds_bytes(TraceArgs& a, int words, size_t elem, bool mtl_lds, bool 
     const size_t want = std::min<size_t>((size_t)a.max_depth, (budget - 12 * slot) / level);
     if (TPT_RECORDS_FIRST ? (slots * slot + want * level > budget) : (slots * slot + 2 * level > budget))
         slots = std::min(slots, std::max<size_t>(12, ((budget - want * level) / slot) & ~(size_t)1));   // even
-    const size_t stack = ((slots + 1) / 2 * 2 * slot + 15) / 16 * 16;   // even slot count (paired u16 layout)
+    const size_t stack = quad ? ((slots + 3) / 4 * 4 * slot + 15) / 16 * 16
+                              : ((slots + 1) / 2 * 2 * slot + 15) / 16 * 16;   // even slot count (paired u16 layout)
     size_t levels = (budget - stack) / level;
     if (levels > (size_t)a.max_depth) levels = (size_t)a.max_depth;
     size_t nodes = wide ? (budget - stack - levels * level) / 128 : 0;
@@ -1181,6 +1221,14 @@ static void use_tile_pool(TraceArgs& a, dim3& grid, size_t& lds) {
     }
     a.lds_pool_offset = (int)((lds + 15) / 16 * 16);
     lds = (size_t)a.lds_pool_offset + 16;
+}
+
+bool trace_quad_fits(const TraceArgs& a_in) {
+    TraceArgs a = a_in;
+    const bool small = (2 * (size_t)a.n_faces - 1) <= 65535;
+    const bool mtl_lds = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
+    trace_lds_bytes(a, 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudgetQuad, true);
+    return rec_words(a.n_lights, a.n_materials) == 2 && a.stack_lds_slots >= a.stack_depth + 3;
 }
 
 hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
@@ -1222,6 +1270,23 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     }
     const bool lights = rec_words(a.n_lights, a.n_materials) == 5;
     const bool mtl_lds = (size_t)(a.n_materials + 1) * 2 * sizeof(float4) <= kLdsMtlMax;
+    if (a.quad) {
+        // four lanes per pixel: 8x8-pixel workgroups; the quads' stacks must lie in
+        // LDS whole (the host checked lights == 0)
+        grid = a.tile_list ? dim3(a.n_tiles, 1)
+                           : dim3((a.width + 7) / 8, ((a.band_height + 7) / 8) * (a.n_frames > 0 ? a.n_frames : 1));
+        a.xcd_run = 0;
+        const size_t lds = trace_lds_bytes(a, 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudgetQuad, true);
+        if (lights || a.stack_lds_slots < a.stack_depth + 3) return hipErrorInvalidValue;
+        if (mtl_lds) {
+            if (small) launch_quad<true, uint16_t>(a, grid, lds, s);
+            else launch_quad<true, int>(a, grid, lds, s);
+        } else {
+            if (small) launch_quad<false, uint16_t>(a, grid, lds, s);
+            else launch_quad<false, int>(a, grid, lds, s);
+        }
+        return hipGetLastError();
+    }
     // pair mode: delta lights (shadow rays to hand off), packed probe ids
     const bool pair = a.pair && lights && a.n_lights > 0 && (a.n_materials + 1) < (int)kNoProbe;
     if (pair) {
@@ -1236,8 +1301,9 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
         }
         return hipGetLastError();
     }
+    if (a.tile_list) grid = dim3(a.n_tiles, 1);
     // pixel pool; its LDS counter comes out of the budget
-    const bool use_pool = TPT_TILE_POOL && !a.drained;
+    const bool use_pool = TPT_TILE_POOL && !a.drained && !a.tile_list && !a.pix_cost;
     size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudget - (use_pool ? 16 : 0));
     if (use_pool) use_tile_pool(a, grid, lds);
     if (lights) {
@@ -1263,13 +1329,15 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
 // Lone-wave step latency (tpt_debug_step_latency; DESIGN.md section 6, "The
 // drained chain"): ONE 64-lane wave walks up to 64 rays with the production
 // closest-hit traversal (4-wide ordered visits, leaves tested when reached, as
-// k_trace_rays mode 1 minus the sliver pass), its 4-wide nodes read from global
+// k_trace_rays mode 1; the sliver pass after the timed walk), its 4-wide nodes read from global
 // memory (nodes_lds 0, what k_trace does) or from a copy of the first
 // nodes_lds nodes in LDS (the whole main tree: every visit an LDS read), the
 // stack in LDS either way.  out[4 * lane]: this lane's visits + leaf tests,
 // the wave's loop iterations, the wave's shader cycles (s_memtime) for the
 // walk, the hit fid.
 constexpr int kLatStackSlots = 64;
+// LaneStack's [slot][lane] layout has a 256-lane row per slot (stack_slot_offset)
+constexpr size_t kLatStackBytes = (size_t)kLatStackSlots * 256 * sizeof(int);
 __global__ __launch_bounds__(64) void k_step_latency(TraceArgs a, uint32_t n, const float* __restrict__ o,
                                                      const float* __restrict__ d, int nodes_lds,
                                                      unsigned long long* __restrict__ out) {
@@ -1332,14 +1400,75 @@ __global__ __launch_bounds__(64) void k_step_latency(TraceArgs a, uint32_t n, co
     }
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    uint32_t c_leaf = 0;
+    if (a.n_sliver_groups > 0 && r.fin) sliver_pass(r, a, c_leaf);   // (untimed) the render's hit
     out[4 * lane] = steps;
     out[4 * lane + 1] = iters;
     out[4 * lane + 2] = t1 - t0;
     out[4 * lane + 3] = (unsigned long long)(long long)r.fid;
 }
+
+// The same walk with FOUR lanes per ray (nodes_lds < 0; DESIGN.md section 6,
+// "Four lanes per ray"): ONE wave, up to 16 rays, ray q on lanes 4q..4q+3 with
+// its traversal state replicated, each 4-wide visit split over the quad
+// (inner_visit4_quad).  out[4 * q]: ray q's node visits, the wave's iterations,
+// the wave's shader cycles, the hit fid.
+__global__ __launch_bounds__(64) void k_step_latency_quad(TraceArgs a, uint32_t n, const float* __restrict__ o,
+                                                          const float* __restrict__ d,
+                                                          unsigned long long* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const int lane = threadIdx.x, q = lane >> 2, k = lane & 3;
+    LaneStack<int, true> stk;
+    stk.lds = (TPT_LDS int*)lds + 4 * q;   // the quad's four columns
+    stk.nlds = kLatStackSlots;
+    const int nint = a.n_faces - 1;
+    const bool active = (uint32_t)q < n;
+    Trav r;
+    trav_begin(r, active ? v3(o[3 * q], o[3 * q + 1], o[3 * q + 2]) : v3(0.0f, 0.0f, 0.0f),
+               active ? v3(d[3 * q], d[3 * q + 1], d[3 * q + 2]) : v3(1.0f, 1.0f, 1.0f), TM_CLOSEST,
+               a.boxes_finite != 0, a.emit_root, a.cull_eps, false);
+    if (!active || !r.fin) r.node = -1;   // finite rays only (chords, camera rays)
+    unsigned long long steps = 0, iters = 0;
+    uint32_t c_leaf = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    while (__ballot(r.node >= 0) != 0ull) {
+        ++iters;
+        if (r.node >= 0) {
+            ++steps;
+            if (r.node >= nint) {   // a one-leaf tree
+                leaf_test<true>(r, a.tri, r.node - nint, a.cull_eps);
+                r.node = -1;
+            } else {
+                bool stop;
+                int next = inner_visit4_quad(r, a.inner4, a.tri, nint, a.cull_eps, stk, r.sp, stop, c_leaf);
+                if (stop || r.sp > a.stack_depth) {
+                    r.sp = 0;
+                    next = -1;
+                }
+                r.node = next >= 0 ? next : (r.sp == 0 ? -1 : stk.get(--r.sp));
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (a.n_sliver_groups > 0 && r.fin) sliver_pass(r, a, c_leaf);   // (untimed) the render's hit
+    if (k == 0) {
+        out[4 * q] = steps;
+        out[4 * q + 1] = iters;
+        out[4 * q + 2] = t1 - t0;
+        out[4 * q + 3] = (unsigned long long)(long long)r.fid;
+    }
+}
+
 hipError_t launch_step_latency_ptr(const void* a, uint32_t n, const float* o, const float* d, int nodes_lds,
                                    unsigned long long* out, hipStream_t s) {
-    const size_t lds = (size_t)nodes_lds * 128 + (size_t)kLatStackSlots * 64 * sizeof(int);
+    if (nodes_lds < 0) {   // four lanes per ray
+        hipLaunchKernelGGL(k_step_latency_quad, dim3(1), dim3(64), kLatStackBytes, s,
+                           *static_cast<const TraceArgs*>(a), n, o, d, out);
+        return hipGetLastError();
+    }
+    const size_t lds = (size_t)nodes_lds * 128 + kLatStackBytes;
     hipLaunchKernelGGL(k_step_latency, dim3(1), dim3(64), lds, s, *static_cast<const TraceArgs*>(a), n, o, d,
                        nodes_lds, out);
     return hipGetLastError();

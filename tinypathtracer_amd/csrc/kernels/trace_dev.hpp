@@ -62,6 +62,9 @@
 // DRAIN variants (launches that cannot fill the chip: a few waves per SIMD anyway)
 #define TPT_TRACE_WAVES_DRAIN 4
 #endif
+#ifndef TPT_TRACE_WAVES_QUAD
+#define TPT_TRACE_WAVES_QUAD 4   // four lanes per pixel (k_trace QUAD)
+#endif
 #ifndef TPT_GRAZE_HIT   // the grazing-hit rule (Culling: "Grazing hits"); 0 only to measure its cost
 #define TPT_GRAZE_HIT 1
 #endif
@@ -339,17 +342,23 @@ __device__ __forceinline__ int stack_slot_offset(int i) {
     return i * 256;
 }
 
-template <typename StackT>
+// QS (four lanes per ray): one stack per quad, in its four lanes' columns --
+// slot i at row i / 4, column 4q + i % 4 -- a quarter of the rows
+template <typename StackT, bool QS = false>
 struct LaneStack {
-    TPT_LDS StackT* lds;   // this lane's base: slot i at lds[stack_slot_offset<StackT>(i)]
+    TPT_LDS StackT* lds;   // this lane's (QS: its quad's first lane's) base: slot i at lds[off(i)]
     int nlds;
     StackT deep[kMaxStackSlots];
+    __device__ static __forceinline__ int off(int i) {
+        if constexpr (QS) return (i >> 2) * 256 + (i & 3);
+        else return stack_slot_offset<StackT>(i);
+    }
     __device__ __forceinline__ void put(int i, int v) {
-        if (i < nlds) lds[stack_slot_offset<StackT>(i)] = (StackT)v;
+        if (i < nlds) lds[off(i)] = (StackT)v;
         else deep[i - nlds] = (StackT)v;
     }
     __device__ __forceinline__ int get(int i) const {
-        return i < nlds ? (int)lds[stack_slot_offset<StackT>(i)] : (int)deep[i - nlds];
+        return i < nlds ? (int)lds[off(i)] : (int)deep[i - nlds];
     }
 };
 
@@ -366,12 +375,12 @@ __device__ __forceinline__ float4 lds_f4(const TPT_LDS LdsF4* p) { return make_f
 // (packed v_pk_add/v_pk_mul slab math was measured 17 % slower: register-pair
 // constraints outweigh the halved instruction count)
 
-template <typename StackT>
+template <typename StackT, bool QS>
 __device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q1, float4 q2, float4 q3, float4 q4,
-                                              float4 q5, float4 q6, LaneStack<StackT>& stk, int& sp);
-template <typename StackT>
+                                              float4 q5, float4 q6, LaneStack<StackT, QS>& stk, int& sp);
+template <typename StackT, bool QS>
 __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restrict__ inner4,
-                                            const TPT_LDS LdsF4* snodes, int nlds_nodes, LaneStack<StackT>& stk,
+                                            const TPT_LDS LdsF4* snodes, int nlds_nodes, LaneStack<StackT, QS>& stk,
                                             int& sp) {
     float4 q0, q1, q2, q3, q4, q5, q6;
     if (TPT_LDS_NODES_MAX > 0 && r.node < nlds_nodes) {   // top levels, staged in LDS at kernel start
@@ -396,9 +405,9 @@ __device__ __forceinline__ int inner_visit4(const Trav& r, const float4* __restr
     return inner_visit4_q(r, q0, q1, q2, q3, q4, q5, q6, stk, sp);
 }
 // the visit's arithmetic on the node's seven float4 (from global memory or LDS)
-template <typename StackT>
+template <typename StackT, bool QS>
 __device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q1, float4 q2, float4 q3, float4 q4,
-                                              float4 q5, float4 q6, LaneStack<StackT>& stk, int& sp) {
+                                              float4 q5, float4 q6, LaneStack<StackT, QS>& stk, int& sp) {
     float k0, k1, k2, k3, e0, e1, e2, e3;
     slab_minmax(r.o, r.inv, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, k0, e0);
     slab_minmax(r.o, r.inv, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, k1, e1);
@@ -446,9 +455,9 @@ __device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q
     const int np = m > 0 ? m - 1 : 0;
     const int v0 = np == 3 ? i3 : (np == 2 ? i2 : i1), v1 = np == 3 ? i2 : i1;
     if (sp + 3 <= stk.nlds) {
-        stk.lds[stack_slot_offset<StackT>(sp)] = (StackT)v0;
-        stk.lds[stack_slot_offset<StackT>(sp + 1)] = (StackT)v1;
-        stk.lds[stack_slot_offset<StackT>(sp + 2)] = (StackT)i1;
+        stk.lds[stk.off(sp)] = (StackT)v0;
+        stk.lds[stk.off(sp + 1)] = (StackT)v1;
+        stk.lds[stk.off(sp + 2)] = (StackT)i1;
     } else {
         stk.put(sp, v0);
         stk.put(sp + 1, v1);
@@ -500,6 +509,87 @@ template <bool ORDERED>
 __device__ __forceinline__ bool leaf_test(Trav& r, const float4* __restrict__ tri, int pos, float cull_eps) {
     const TriQ tq = tri_load(tri, pos);
     return leaf_test_q<ORDERED>(r, tq.q0, tq.q1, tq.q2, pos, cull_eps);
+}
+
+// Four lanes per ray (k_trace QUAD variants, tpt_debug_step_latency mode 2;
+// DESIGN.md section 6, "Four lanes per ray").  The ray's traversal state is
+// replicated on lanes 4q..4q+3 (every lane computes the same path); a 4-wide
+// visit is split over them: lane k loads and tests child k alone (its 24-byte
+// box, its link), leaf children are tested at once, each by its own lane, and
+// the quad keeps the best hit under the tie rule (least t, then the larger leaf
+// position: the order-independent result of the one-lane walk, so the hit is
+// the same); the internal children that pass -- against the bound the leaves
+// left -- are ranked by slab entry across the quad (DPP), the nearest is
+// returned and the others are pushed farthest-first, each by its own lane, into
+// the quad's stack (LaneStack QS).  A node passes the culls of the final
+// bound whenever it passes them in the one-lane walk, so the sliver pass's
+// premise holds.
+template <int CTRL>
+__device__ __forceinline__ int quad_mov(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float quad_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+constexpr int kQuadXor1 = 0xb1, kQuadXor2 = 0x4e;   // quad_perm [1,0,3,2], [2,3,0,1]
+// one butterfly step of the quad's best-hit reduction
+template <int CTRL>
+__device__ __forceinline__ void quad_best(Trav& r) {
+    const float t2 = quad_mov<CTRL>(r.t), u2 = quad_mov<CTRL>(r.u), v2 = quad_mov<CTRL>(r.v), l2 = quad_mov<CTRL>(r.lim);
+    const int p2 = quad_mov<CTRL>(r.hpos), f2 = quad_mov<CTRL>(r.fid), m2 = quad_mov<CTRL>(r.mode);
+    const bool take = (t2 < r.t) | ((t2 == r.t) & (r.hpos >= 0) & (p2 > r.hpos));
+    r.t = take ? t2 : r.t;
+    r.u = take ? u2 : r.u;
+    r.v = take ? v2 : r.v;
+    r.lim = take ? l2 : r.lim;
+    r.hpos = take ? p2 : r.hpos;
+    r.fid = take ? f2 : r.fid;
+    r.mode = take ? m2 : r.mode;
+}
+// The split visit of 4-wide node r.node (finite rays): returns the child to
+// descend into (-1: none); stop when a leaf test ends an any-hit / occlusion walk.
+template <typename StackT, bool QS>
+__device__ __forceinline__ int inner_visit4_quad(Trav& r, const float4* __restrict__ inner4,
+                                                 const float4* __restrict__ tri, int nint, float cull_eps,
+                                                 LaneStack<StackT, QS>& stk, int& sp, bool& stop, uint32_t& c_leaf) {
+    const int lane = (int)__lane_id(), k = lane & 3;
+    const float* nf = (const float*)(inner4 + 8 * (size_t)r.node);
+    const float2 b0 = *(const float2*)(nf + 6 * k), b1 = *(const float2*)(nf + 6 * k + 2),
+                 b2 = *(const float2*)(nf + 6 * k + 4);
+    const int link = ((const int*)nf)[24 + k];
+    float kk, ee;
+    slab_minmax(r.o, r.inv, b0.x, b0.y, b1.x, b1.y, b2.x, b2.y, kk, ee);
+    const float hd = 0.5f * kDelta;
+    const int id = link & kLinkMask;
+    const bool h = (link >= 0) & (fmaxf(kk, hd) <= fminf(ee, r.lim));
+    const bool lf = h & (id >= nint);
+    stop = false;
+    if (__ballot(lf) != 0ull) {
+        int s = 0;
+        if (lf) {
+            ++c_leaf;
+            s = leaf_test<true>(r, tri, id - nint, cull_eps) ? 1 : 0;
+        }
+        quad_best<kQuadXor1>(r);
+        quad_best<kQuadXor2>(r);
+        s |= quad_mov<kQuadXor1>(s);
+        s |= quad_mov<kQuadXor2>(s);
+        stop = s != 0;
+    }
+    // internal children against the bound the leaves left
+    const bool in = !stop & h & (id < nint) & (fmaxf(kk, hd) <= fminf(ee, r.lim));
+    const float key = in ? kk : __builtin_inff();
+    const float c0 = quad_mov<0x00>(key), c1 = quad_mov<0x55>(key), c2 = quad_mov<0xaa>(key), c3 = quad_mov<0xff>(key);
+    const int rank = ((c0 < key) | ((c0 == key) & (0 < k))) + ((c1 < key) | ((c1 == key) & (1 < k))) +
+                     ((c2 < key) | ((c2 == key) & (2 < k))) + ((c3 < key) | ((c3 == key) & (3 < k)));
+    const int n_in = __popcll((__ballot(in) >> (lane & ~3)) & 0xfull);
+    if (in & (rank > 0)) stk.put(sp + n_in - 1 - rank, id);
+    int near = (in & (rank == 0)) ? id : -1;
+    near = max(near, quad_mov<kQuadXor1>(near));
+    near = max(near, quad_mov<kQuadXor2>(near));
+    sp += n_in > 0 ? n_in - 1 : 0;
+    return near;
 }
 
 // Probe pass 1 over an emissive-triangle tree that is a single 4-wide node of

@@ -68,7 +68,42 @@ def main():
                                 "cycles_per_iteration": round(cyc / max(iters, 1), 1)}
                     print(f"{key:45s} iterations {iters:5d}  busiest lane {int(steps.max()):4d} steps  "
                           f"mean {steps.mean():6.2f}  cycles/iteration {cyc / max(iters, 1):7.1f}")
-    print(json.dumps({"scene": name, "results": out}))
+    # four lanes per ray (mode 2) against one lane per ray on the same rays: the
+    # wave's whole walk in cycles (the chain latency of its slowest ray) and the hits
+    quad = {}
+    for kind in ("glass chords", "camera"):
+        for nr in (16, 4, 1):
+            # (the four-lane walk takes finite rays only; a direction with a zero
+            # component has an infinite 1/d and takes the binary path in the render)
+            o, dr = rays(s, d, kind, 8 * nr, rng)
+            keep = np.nonzero(np.all(dr != 0.0, axis=1))[0][:nr]
+            o, dr = o[keep], dr[keep]
+            res = {}
+            for mode, mname in ((0, "one lane"), (2, "four lanes")):
+                best = None
+                for _ in range(5):
+                    steps, iters, cyc, fid = d.step_latency(o, dr, mode, 0)
+                    if best is None or cyc < best[2]:
+                        best = (steps, iters, cyc, fid)
+                res[mname] = best
+            same = bool(np.array_equal(res["one lane"][3], res["four lanes"][3]))
+            if not same:
+                bad = np.nonzero(res["one lane"][3] != res["four lanes"][3])[0]
+                hit0, _, _ = d.trace_rays(o[bad], dr[bad], mode=0)
+                hit1, _, _ = d.trace_rays(o[bad], dr[bad], mode=1)
+                print("  differing rays", bad.tolist(), "one lane", res["one lane"][3][bad].tolist(), "four lanes",
+                      res["four lanes"][3][bad].tolist(), "reference order", np.asarray(hit0).tolist(),
+                      "render", np.asarray(hit1).tolist())
+            c1, c4 = res["one lane"][2], res["four lanes"][2]
+            key = f"{kind} x{nr}"
+            quad[key] = {"one_lane_cycles": c1, "four_lane_cycles": c4, "ratio": round(c4 / max(c1, 1), 3),
+                         "one_lane_busiest_steps": int(res["one lane"][0].max()),
+                         "four_lane_busiest_visits": int(res["four lanes"][0].max()),
+                         "one_lane_iterations": res["one lane"][1], "four_lane_iterations": res["four lanes"][1],
+                         "same_hits": same}
+            print(f"{key:22s} one lane {c1:7d} cycles ({res['one lane'][1]:4d} iterations)  four lanes {c4:7d} "
+                  f"({res['four lanes'][1]:4d} iterations)  ratio {c4 / max(c1, 1):.3f}  same hits {same}")
+    print(json.dumps({"scene": name, "results": out, "four_lanes": quad}))
     d.close()
 
 
