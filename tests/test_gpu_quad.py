@@ -137,25 +137,21 @@ def test_quad_full_size_c2_strong_split_bit_identical(built):
     assert rays == st["traversals"]
 
 
-@pytest.mark.parametrize("frac,cap", [("0.5", "160"), ("0", "100000"), ("0.9", "3"), ("2", "160")])
-def test_hybrid_lanes_per_pixel_bit_identical(built, monkeypatch, frac, cap):
-    """lanes_per_pixel 0 on a drained launch (render_hybrid): the first 1/16 of the
-    samples one lane per pixel with each pixel's rays counted, then the heaviest
-    tiles four lanes per pixel and the rest one lane, side by side.  Any split
-    (every tile heavy, a few, none) gives the one-lane frame bit for bit."""
-    monkeypatch.setenv("TPT_HYBRID_FRAC", frac)
-    monkeypatch.setenv("TPT_HYBRID_CAP", cap)
+def test_auto_lanes_bit_identical_on_small_and_large_launches(built):
+    """lanes_per_pixel 0 picks four lanes per pixel for launches with no more pixels
+    than the chip's resident lanes (327,680) and one lane above: either way the
+    one-lane frame, bit for bit, with the same rays."""
     s, d, o = built["box"]
-    W, H, spp = 200, 120, 48
-    rad0, fb0, st0 = _render(s, d, W, H, spp, 8, None, 0)
-    rad1, fb1, st1 = _render(s, d, W, H, spp, 8, None, 1)
-    assert _same(rad0, rad1)
-    assert np.array_equal(fb0, fb1)
-    for k in STATS:
-        assert st0[k] == st1[k], k
-    acc = np.zeros_like(rad1)   # the strong-scaled split: each band set drained
-    for b in range(3):
-        part, _, _ = _render(s, d, W, H, spp, 8, None, 0, band=(16, 3, b))
-        rows = [y for y in range(H) if (y // 16) % 3 == b]
+    for W, H, spp in ((200, 120, 16), (1920, 1080, 2)):
+        rad0, fb0, st0 = _render(s, d, W, H, spp, 8, None, 0)
+        rad1, fb1, st1 = _render(s, d, W, H, spp, 8, None, 1)
+        assert _same(rad0, rad1)
+        assert np.array_equal(fb0, fb1)
+        for k in STATS:
+            assert st0[k] == st1[k], k
+    acc = np.zeros((1080, 1920, 3), np.float32)   # the strong-scaled split at N = 8: four lanes (auto)
+    for b in range(8):
+        part, _, _ = _render(s, d, 1920, 1080, 2, 8, None, 0, band=(16, 8, b))
+        rows = [y for y in range(1080) if (y // 16) % 8 == b]
         acc[rows] = part[rows]
     assert _same(acc, rad1)

@@ -106,10 +106,6 @@ struct TraceArgs {
     int32_t pair;                        // 1: pair mode (two lanes per pixel, shadow rays on the side lane)
     int32_t drained;                     // 1: the launch cannot fill the chip (latency-oriented DRAIN variants)
     int32_t quad;                        // 1: four lanes per pixel, each node visit split over them (k_trace QUAD)
-    const int32_t* tile_list;            // non-null: workgroup b renders tile tile_list[b] = row block << 16 | column
-                                         //    (16x16 tiles, QUAD 8x8; one frame; no pixel pool)
-    int32_t n_tiles;                     // entries of tile_list (the grid)
-    uint32_t* pix_cost;                  // non-null: each pixel's rays in this launch (one lane per pixel, no pool)
     int32_t xcd_run;                     // > 0: workgroup tiles dealt to XCDs in runs of this many (k_trace)
     int32_t tile_pool;                   // 1: each workgroup renders two adjacent tiles, the second as a pixel
                                          //    pool its finished lanes draw from (k_trace; set by launch_trace)

@@ -408,10 +408,6 @@ struct tpt_scene {
     DevBuf<float4> wf_q0, wf_q1, wf_hit;
     HostPinned<uint32_t> wf_count;
     hipEvent_t wf_ev[2] = {nullptr, nullptr};
-    // hybrid launches (render_hybrid): each pixel's rays in the measuring launch,
-    // and the two tile lists
-    DevBuf<uint32_t> pix_cost;
-    DevBuf<int32_t> tile_list;
 
     ~tpt_scene() {
         DeviceGuard g(device);
@@ -1183,118 +1179,6 @@ static tpt_status render_wavefront(tpt_scene* s, const tpt::TraceArgs& a, const 
     return TPT_OK;
 }
 
-// Hybrid lanes per pixel for drained launches ("Four lanes
-// per ray"; lanes_per_pixel 0 = auto).  A launch with fewer pixels than the chip
-// has lanes is its heaviest tiles' serial chains.  Four lanes per pixel shorten
-// a chain (each 4-wide visit split over the quad) at four times the lanes per
-// pixel, which only the heavy tiles can afford.  So: the first 1/16 of the
-// samples run one lane per pixel and count each pixel's rays (pix_cost); a tile
-// costs its heaviest pixel; the tiles within `frac` of the heaviest (at most
-// `cap` of them) run the remaining samples with four lanes per pixel, the rest
-// with one, the two launches side by side on two streams.  Each pixel's samples
-// still run in order on its own XORWOW stream (RNG state and sums persist
-// between launches), so the frame is bit-identical to one launch.
-static tpt_status render_hybrid(tpt_scene* s, const tpt::TraceArgs& a, const tpt_params* p, int bh, int band_rows,
-                                int band_count, double& trace_ms, double& kernel_ms, int& launches) {
-    hipStream_t st = s->stream;
-    const int W = p->width, H = p->height;
-    const int spp0 = std::max(1, p->spp / 16), rest = p->spp - spp0;
-    double frac = 0.5;
-    int cap = 160;
-    if (const char* e = std::getenv("TPT_HYBRID_FRAC")) frac = std::atof(e);
-    if (const char* e = std::getenv("TPT_HYBRID_CAP")) cap = std::atoi(e);
-    auto launch = [&](const tpt::TraceArgs& ak, hipStream_t q) {
-        return (p->flags & TPT_FLAG_FAST) ? tpt_fast::launch_trace_ptr(&ak, q) : tpt::launch_trace(ak, q);
-    };
-    HIP_OR_FAIL(s->pix_cost.alloc((size_t)W * (size_t)H));
-    HIP_OR_FAIL(s->ensure_launch_events(6));
-    HIP_OR_FAIL(s->ensure_pipe(2));
-    tpt::TraceArgs a1 = a;
-    a1.samples = spp0;
-    a1.quad = 0;
-    a1.pix_cost = s->pix_cost.p;
-    HIP_OR_FAIL(hipEventRecord(s->lev[0], st));
-    HIP_OR_FAIL(launch(a1, st));
-    HIP_OR_FAIL(hipEventRecord(s->lev[1], st));
-    int nev = 1;
-    if (rest > 0) {
-        std::vector<uint32_t> cost((size_t)W * (size_t)H);
-        HIP_OR_FAIL(hipStreamSynchronize(st));
-        HIP_OR_FAIL(hipMemcpy(cost.data(), s->pix_cost.p, cost.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        const int gx = (W + 15) / 16, gy = (bh + 15) / 16;
-        std::vector<uint32_t> tc((size_t)gx * gy, 0);
-        for (int ly = 0; ly < bh; ++ly) {
-            const int y = ((ly / band_rows) * band_count + p->band_index) * band_rows + ly % band_rows;
-            if (y >= H) continue;
-            const uint32_t* row = cost.data() + (size_t)y * W;
-            uint32_t* t = tc.data() + (size_t)(ly / 16) * gx;
-            for (int x = 0; x < W; ++x) t[x / 16] = std::max(t[x / 16], row[x]);
-        }
-        std::vector<int> idx(tc.size());
-        for (size_t i = 0; i < idx.size(); ++i) idx[i] = (int)i;
-        std::stable_sort(idx.begin(), idx.end(), [&](int u, int v) { return tc[u] > tc[v]; });
-        const double thr = frac * (double)(tc.empty() ? 0u : tc[idx[0]]);
-        std::vector<char> heavy(tc.size(), 0);
-        for (size_t i = 0; i < idx.size() && (int)i < cap && (double)tc[idx[i]] >= thr && tc[idx[i]] > 0; ++i)
-            heavy[idx[i]] = 1;
-        // lists: light 16x16 tiles (one lane per pixel), heavy ones as four 8x8 quad tiles
-        std::vector<int32_t> light, quad;
-        for (int ty = 0; ty < gy; ++ty)
-            for (int tx = 0; tx < gx; ++tx) {
-                if (!heavy[(size_t)ty * gx + tx]) {
-                    light.push_back((ty << 16) | tx);
-                } else {
-                    for (int j = 0; j < 2; ++j)
-                        for (int i = 0; i < 2; ++i) quad.push_back(((2 * ty + j) << 16) | (2 * tx + i));
-                }
-            }
-        HIP_OR_FAIL(s->tile_list.alloc((size_t)((W + 15) / 16) * (size_t)((H + 15) / 16) * 4));
-        HIP_OR_FAIL(hipMemcpy(s->tile_list.p, light.data(), light.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-        HIP_OR_FAIL(hipMemcpy(s->tile_list.p + light.size(), quad.data(), quad.size() * sizeof(int32_t),
-                              hipMemcpyHostToDevice));
-        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[0], st));
-        hipStream_t q0 = s->pipe[0], q1 = s->pipe[1];
-        HIP_OR_FAIL(hipStreamWaitEvent(q0, s->pipe_ev[0], 0));
-        HIP_OR_FAIL(hipStreamWaitEvent(q1, s->pipe_ev[0], 0));
-        tpt::TraceArgs al = a, ah = a;
-        al.samples = ah.samples = rest;
-        al.quad = 0;
-        al.tile_list = s->tile_list.p;
-        al.n_tiles = (int32_t)light.size();
-        ah.quad = 1;
-        ah.tile_list = s->tile_list.p + light.size();
-        ah.n_tiles = (int32_t)quad.size();
-        // the heavy tiles first: their chains are the frame's
-        if (!quad.empty()) {
-            HIP_OR_FAIL(hipEventRecord(s->lev[2], q1));
-            HIP_OR_FAIL(launch(ah, q1));
-            HIP_OR_FAIL(hipEventRecord(s->lev[3], q1));
-            ++nev;
-        }
-        if (!light.empty()) {
-            HIP_OR_FAIL(hipEventRecord(s->lev[2 * nev], q0));
-            HIP_OR_FAIL(launch(al, q0));
-            HIP_OR_FAIL(hipEventRecord(s->lev[2 * nev + 1], q0));
-            ++nev;
-        }
-        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[1], q0));
-        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[2], q1));
-        HIP_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[1], 0));
-        HIP_OR_FAIL(hipStreamWaitEvent(st, s->pipe_ev[2], 0));
-    }
-    HIP_OR_FAIL(hipEventRecord(s->ev[2], st));
-    HIP_OR_FAIL(hipEventSynchronize(s->ev[2]));
-    float ms = 0.0f;
-    HIP_OR_FAIL(hipEventElapsedTime(&ms, s->ev[1], s->ev[2]));
-    trace_ms = ms;
-    for (int j = 0; j < nev; ++j) {
-        HIP_OR_FAIL(hipEventElapsedTime(&ms, s->lev[2 * j], s->lev[2 * j + 1]));
-        kernel_ms += ms;
-        ++launches;
-    }
-    return TPT_OK;
-}
-
 tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera* cam, const tpt_params* p,
                              int32_t n_frames, const uint64_t* seeds, float* const* radiance_outs,
                              uint8_t* const* bgra_outs, tpt_stats* stats) {
@@ -1367,12 +1251,6 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
 
     if (p->lanes_per_pixel < 0 || p->lanes_per_pixel > 4 || p->lanes_per_pixel == 3)
         return fail(TPT_ERR_INVALID_ARG, "lanes_per_pixel: 0, 1, 2 or 4");
-    // four lanes per pixel ("Four lanes per ray"): every
-    // lane of a quad runs the pixel's path, each 4-wide visit split over them;
-    // the one-lane kernel logic, so no delta lights, env IS or reference order
-    a.quad = p->lanes_per_pixel == 4 ? 1 : 0;
-    if (a.quad && (s->n_lights > 0 || a.env_is || (p->flags & TPT_FLAG_REF_ORDER)))
-        return fail(TPT_ERR_INVALID_ARG, "lanes_per_pixel 4: scenes without delta lights, no env IS, ordered traversal");
     // auto: pair mode wherever there are shadow rays to hand off (C3 1080p 4096 spp:
     // 4.91 -> 6.65 Grays/s); the kernel falls back to one lane per pixel otherwise
     // (A15 env IS: the env shadow ray of every diffuse bounce is the side lane's job too)
@@ -1384,6 +1262,21 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // 8 -> 6.44, 2..12 within 6.2-6.6 Grays/s; C2 single-lane: 16-24 best).
     const bool pair_kernel = a.pair && (s->n_lights > 0 || a.env_is) && (s->n_materials + 1) < 0x7fff &&
                              !(p->flags & TPT_FLAG_REF_ORDER);
+    // Four lanes per pixel ("Four lanes per ray"): every lane
+    // of a quad runs the pixel's path, each 4-wide visit split over them -- the
+    // one-lane kernel logic, so no delta lights, env IS or reference order, and the
+    // quads' stacks in LDS.  Auto on launches with no more pixels than the chip's
+    // resident lanes (256 CUs x 4 SIMDs x 5 waves x 64 = 327,680), which are their
+    // heaviest tiles' serial chains: strong-scaled C2 at N = 8 (259 K pixels per
+    // GPU, slowest rank) 314 -> 250 ms; at N = 4 (518 K) four lanes lose (463 vs
+    // 328 ms: four times the waves), so the chip is the bound.
+    const double launch_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
+    const bool quad_ok = p->lanes_per_pixel != 2 && s->n_lights == 0 && !a.env_is &&
+                         !(p->flags & TPT_FLAG_REF_ORDER) && tpt::trace_quad_fits(a);
+    if (p->lanes_per_pixel == 4 && !quad_ok)
+        return fail(TPT_ERR_INVALID_ARG,
+                    "lanes_per_pixel 4: scenes without delta lights, no env IS, ordered traversal, stacks in LDS");
+    a.quad = (p->lanes_per_pixel == 4 || (p->lanes_per_pixel == 0 && launch_pix <= 327680.0 && quad_ok)) ? 1 : 0;
     // the trace grid's y extent is (band row blocks) x frames: 8-row workgroups in
     // pair mode, 16 otherwise (launch_trace)
     {
@@ -1396,7 +1289,6 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // images) is bound by its heaviest waves' chains, not by throughput: batch
     // the shading passes harder (C2 rank 0 of 8: refill 24 318 ms, 4: 276 ms;
     // rank 0 of 4: flat).
-    const double launch_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
     const bool drained = launch_pix < 2.0 * 327680.0;
     // Shallow trees (few triangles) make a traversal short against a shading
     // pass, so passes are batched harder there: tir (6 triangles) refill 16
@@ -1452,19 +1344,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     size_t dbg_words = 0;
     if ((p->flags & TPT_FLAG_WAVEFRONT) && (p->flags & (TPT_FLAG_FAST | TPT_FLAG_APPROX_CULL)))
         return fail(TPT_ERR_INVALID_ARG, "TPT_FLAG_WAVEFRONT runs the exact traversal only");
-    // hybrid lanes per pixel (render_hybrid): drained one-frame launches of the
-    // one-lane logic, with the automatic schedule; TPT_HYBRID=0 turns it off
-    const char* hyb_env = std::getenv("TPT_HYBRID");
-    const bool hybrid = a.drained && p->lanes_per_pixel == 0 && nf == 1 && !pair_kernel && !a.env_is &&
-                        !(p->flags & TPT_FLAG_REF_ORDER) && p->spp >= 32 && p->spp_per_launch <= 0 &&
-                        p->pipe_sets <= 0 && p->pipe_chunks <= 0 && bh > 0 && !(hyb_env && hyb_env[0] == '0') &&
-                        tpt::trace_quad_fits(a);
     if (p->flags & TPT_FLAG_WAVEFRONT) {   // the wavefront / ray-queue variant (wavefront.hip)
         const tpt_status ws = render_wavefront(s, a, p, n_frames, bh, trace_ms, kernel_ms, launches);
         if (ws != TPT_OK) return ws;
-    } else if (hybrid) {
-        const tpt_status hs = render_hybrid(s, a, p, bh, band_rows, band_count, trace_ms, kernel_ms, launches);
-        if (hs != TPT_OK) return hs;
     } else {
     int chunk = p->spp_per_launch;
     int nset = 1;

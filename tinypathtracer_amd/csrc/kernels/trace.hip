@@ -114,11 +114,6 @@ void k_trace(TraceArgs a) {
     // screen locality of a single frame (node reuse in L1/L2)
     const int nfr = a.n_frames > 0 ? a.n_frames : 1;
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
-    if (a.tile_list) {   // a listed subset of the tiles (host render_hybrid; one frame)
-        const int t = a.tile_list[blockIdx.x];
-        bx = t & 0xffff;
-        by = t >> 16;
-    }
     // XCD runs (scenes larger than an XCD's 4 MiB L2): blocks b and b + 8 share
     // an XCD.  Within each row of workgroups XCD k gets runs of xcd_run
     // adjacent tiles instead of every 8th tile, so its resident tiles see less
@@ -858,7 +853,6 @@ void k_trace(TraceArgs a) {
         g_acc[npix + off] = total.y;
         g_acc[2 * npix + off] = total.z;
     }
-    if (a.pix_cost && pixel && lead) a.pix_cost[off] = c_trav;   // (one lane per pixel, no pool)
     if (!lead) {   // QUAD: the pixel's work is counted once
         c_trav = c_inner = c_wide = c_leaf = c_shade = c_ovf = c_local = 0;
     }
@@ -1273,8 +1267,7 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
     if (a.quad) {
         // four lanes per pixel: 8x8-pixel workgroups; the quads' stacks must lie in
         // LDS whole (the host checked lights == 0)
-        grid = a.tile_list ? dim3(a.n_tiles, 1)
-                           : dim3((a.width + 7) / 8, ((a.band_height + 7) / 8) * (a.n_frames > 0 ? a.n_frames : 1));
+        grid = dim3((a.width + 7) / 8, ((a.band_height + 7) / 8) * (a.n_frames > 0 ? a.n_frames : 1));
         a.xcd_run = 0;
         const size_t lds = trace_lds_bytes(a, 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudgetQuad, true);
         if (lights || a.stack_lds_slots < a.stack_depth + 3) return hipErrorInvalidValue;
@@ -1301,9 +1294,8 @@ hipError_t launch_trace(const TraceArgs& a_in, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    if (a.tile_list) grid = dim3(a.n_tiles, 1);
     // pixel pool; its LDS counter comes out of the budget
-    const bool use_pool = TPT_TILE_POOL && !a.drained && !a.tile_list && !a.pix_cost;
+    const bool use_pool = TPT_TILE_POOL && !a.drained;
     size_t lds = trace_lds_bytes(a, lights ? 5 : 2, small ? 2 : 4, mtl_lds, true, 256, kLdsBudget - (use_pool ? 16 : 0));
     if (use_pool) use_tile_pool(a, grid, lds);
     if (lights) {
