@@ -565,6 +565,19 @@ __device__ __forceinline__ int inner_visit4_quad(Trav& r, const float4* __restri
     const bool h = (link >= 0) & (fmaxf(kk, hd) <= fminf(ee, r.lim));
     const bool lf = h & (id >= nint);
     stop = false;
+#ifndef TPT_QUAD_EARLY
+#define TPT_QUAD_EARLY 1
+#endif
+#if TPT_QUAD_EARLY
+    // the leaf children's triangles in flight while the internal children are ranked
+    // against the bound the node was entered with (strong-scaled C2 at N = 8, 2
+    // interleaved reps: 245.0 / 245.7 ms against 249.8 / 250.1 with the ranking after
+    // the leaf tests, which culls siblings beyond a leaf hit at the cost of the wait)
+    TriQ tq = TriQ{make_float4(0.0f, 0.0f, 0.0f, 0.0f), make_float4(0.0f, 0.0f, 0.0f, 0.0f),
+                   make_float4(0.0f, 0.0f, 0.0f, 0.0f)};
+    if (lf) tq = tri_load(tri, id - nint);
+    const bool in = h & (id < nint);
+#else
     if (__ballot(lf) != 0ull) {
         int s = 0;
         if (lf) {
@@ -579,6 +592,7 @@ __device__ __forceinline__ int inner_visit4_quad(Trav& r, const float4* __restri
     }
     // internal children against the bound the leaves left
     const bool in = !stop & h & (id < nint) & (fmaxf(kk, hd) <= fminf(ee, r.lim));
+#endif
     const float key = in ? kk : __builtin_inff();
     const float c0 = quad_mov<0x00>(key), c1 = quad_mov<0x55>(key), c2 = quad_mov<0xaa>(key), c3 = quad_mov<0xff>(key);
     const int rank = ((c0 < key) | ((c0 == key) & (0 < k))) + ((c1 < key) | ((c1 == key) & (1 < k))) +
@@ -589,6 +603,20 @@ __device__ __forceinline__ int inner_visit4_quad(Trav& r, const float4* __restri
     near = max(near, quad_mov<kQuadXor1>(near));
     near = max(near, quad_mov<kQuadXor2>(near));
     sp += n_in > 0 ? n_in - 1 : 0;
+#if TPT_QUAD_EARLY
+    if (__ballot(lf) != 0ull) {
+        int s = 0;
+        if (lf) {
+            ++c_leaf;
+            s = leaf_test_q<true>(r, tq.q0, tq.q1, tq.q2, id - nint, cull_eps) ? 1 : 0;
+        }
+        quad_best<kQuadXor1>(r);
+        quad_best<kQuadXor2>(r);
+        s |= quad_mov<kQuadXor1>(s);
+        s |= quad_mov<kQuadXor2>(s);
+        stop = s != 0;
+    }
+#endif
     return near;
 }
 
