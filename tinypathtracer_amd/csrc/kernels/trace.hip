@@ -99,7 +99,7 @@ __device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int p
 // bit-identical.  A pixel's sample chain then pays one traversal per bounce
 // instead of 1 + lights, which is what bounds tail-heavy frames (C3).
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
-          bool PAIR = false, bool DRAIN = false, bool QUAD = false>
+          bool PAIR = false, bool DRAIN = false, bool QUAD = false, bool NOEMIT = false>
 __global__ __launch_bounds__(256, ENVIS ? TPT_TRACE_WAVES_IS
                                         : (PAIR ? TPT_TRACE_WAVES_PAIR
                                                 : (QUAD ? TPT_TRACE_WAVES_QUAD
@@ -311,7 +311,7 @@ void k_trace(TraceArgs a) {
             }
         }
 #endif
-        if (TPT_GRAZE_HIT && ORDERED && ts == TS_DONE && phase == PH_PROBE && r.fin && r.fid >= 0 && r.mode == TM_EMIT &&
+        if (TPT_GRAZE_HIT && ORDERED && !NOEMIT && ts == TS_DONE && phase == PH_PROBE && r.fin && r.fid >= 0 && r.mode == TM_EMIT &&
             a.graze && grazing(Surf{a.shade[3 * r.fid + 1].w, a.shade[3 * r.fid + 2].w}, r.d)) {
             // a grazing probe hit (Culling: "Grazing hits"): pass 1 again on the
             // uncull'd binary path, which tests every leaf whose box its line passes
@@ -320,7 +320,7 @@ void k_trace(TraceArgs a) {
             ts = TS_TRAV;
             sl_pend = false;
         }
-        if (ORDERED && ts == TS_DONE && phase == PH_PROBE && r.mode == TM_EMIT && r.fid >= 0) {
+        if (ORDERED && !NOEMIT && ts == TS_DONE && phase == PH_PROBE && r.mode == TM_EMIT && r.fid >= 0) {
             // direct probe, pass 2: the emitter hit stands unless something
             // beats it -- restart from the root keeping its t, position and fid
             r.mode = TM_OCCL;
@@ -399,7 +399,7 @@ void k_trace(TraceArgs a) {
             } else if (ENVIS && phase == PH_ENVSHADOW) {   // env next-event estimate (A15, opt-in)
                 if (r.fid < 0) direct = direct + env_k;
                 lights_next = true;
-            } else if (phase == PH_PROBE) {   // :390-400
+            } else if (!NOEMIT && phase == PH_PROBE) {   // :390-400
                 V3 dl = LIGHTS ? direct : v3(0.0f, 0.0f, 0.0f);
                 uint32_t pm = kNoProbe;
                 if (r.fid >= 0 && r.mode != TM_OCCLUDED) {   // the closest hit (an unbeaten emitter, pass 2)
@@ -476,7 +476,7 @@ void k_trace(TraceArgs a) {
                         float af2;
                         if (!TPT_SHARE_HEMI) hb_ok = false;   // (A/B builds: the frame recomputed)
                         new_direction(rd, nrm, m1.x, m1.y, st, td, af2, hb, hb_ok);
-                        if ((TPT_PROBE_SHORTCUT && ORDERED && !a.any_emitter) ||
+                        if ((TPT_PROBE_SHORTCUT && ORDERED && (NOEMIT || !a.any_emitter)) ||
                             (ORDERED && probe_misses_emitters(a, r.o, td))) {
                             // no triangle emits, or the probe's line passes no emitter's
                             // leaf box: the probe's emitter pass ends with no hit, exactly
@@ -1104,9 +1104,9 @@ hipError_t launch_hot_kat(int op, uint32_t n, const float* in, float* out, hipSt
 }
 
 template <int MAXD, bool ORDERED, bool LIGHTS, bool MTL_LDS, typename StackT, bool ENVIS = false, bool INL = false,
-          bool PAIR = false, bool DRAIN = false, bool QUAD = false>
+          bool PAIR = false, bool DRAIN = false, bool QUAD = false, bool NOEMIT = false>
 static void launch_one(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR, DRAIN, QUAD>), grid,
+    hipLaunchKernelGGL((k_trace<MAXD, ORDERED, LIGHTS, MTL_LDS, StackT, ENVIS, INL, PAIR, DRAIN, QUAD, NOEMIT>), grid,
                        dim3(256), lds, s, a);
 }
 // four lanes per pixel (a.quad): one-lane logic without delta lights
@@ -1123,9 +1123,24 @@ static void launch_quad(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s
 
 // INL: probe pass 1 in the shading pass (an emissive tree of one node); its own
 // variant, so scenes with larger emitter sets keep the leaner kernel.  PAIR:
-// pair mode (delta-light scenes only).
+// pair mode (delta-light scenes only).  NOEMIT (pair variants): no triangle
+// emits, so every direct probe ends in the shading pass (TPT_PROBE_SHORTCUT) and
+// the probe's traversal phases are compiled out -- the pair kernel's registers
+// for C3's and C3 + IS's ball.
+#ifndef TPT_NOEMIT_PAIR
+#define TPT_NOEMIT_PAIR 1
+#endif
 template <bool LIGHTS, bool MTL_LDS, typename StackT, bool PAIR = false, bool ENVIS = false, bool DRAIN = false>
 static void launch_ordered_d(const TraceArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+    if constexpr (PAIR && TPT_NOEMIT_PAIR && TPT_PROBE_SHORTCUT) {
+        if (!a.any_emitter) {
+            if (a.max_depth <= 8)
+                launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR, DRAIN, false, true>(a, grid, lds, s);
+            else
+                launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, false, PAIR, DRAIN, false, true>(a, grid, lds, s);
+            return;
+        }
+    }
     if (TPT_PROBE_INLINE && a.emit_inline) {
         if (a.max_depth <= 8) launch_one<8, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR, DRAIN>(a, grid, lds, s);
         else launch_one<64, true, LIGHTS, MTL_LDS, StackT, ENVIS, true, PAIR, DRAIN>(a, grid, lds, s);
