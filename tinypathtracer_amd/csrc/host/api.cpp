@@ -1299,8 +1299,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // 3 7,911-7,934, 2 7,860-7,983 -> 3; with env IS (the side lane's env sample
     // and shadow ray per diffuse bounce): 8 5,562-5,630, 4 5,745-5,803, 2
     // 5,934-5,970, 1 6,070-6,153 -> 1 (the wave shades only once no lane traverses).
-    a.refill = p->refill > 0 ? std::min(p->refill, 64)
-                             : (pair_kernel ? (a.env_is ? 1 : 3) : (drained ? 4 : full));
+    // Round 5, after the emitter-free pair variants (C3, 2 reps): 4 8,071 / 8,129,
+    // 3 8,185 / 8,156, 2 8,223 / 8,260, 1 8,676 / 8,710 -> 1 without env IS too.
+    a.refill = p->refill > 0 ? std::min(p->refill, 64) : (pair_kernel ? 1 : (drained ? 4 : full));
     a.drained = drained ? 1 : 0;   // latency-oriented kernel variants (trace.hip DRAIN)
     // Parked-leaf batch (speculative leaf postponement): a wave runs its triangle
     // tests once this many lanes are blocked on a parked leaf.  Pair mode has
