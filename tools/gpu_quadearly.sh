@@ -2,6 +2,9 @@
 # Four-lane visit with the leaf children's triangles in flight during the ranking
 # (variants/qe, TPT_QUAD_EARLY=1) against the tree's build: parity of the variant,
 # lone-walk latency, strong-scaled C2 at N = 8 (interleaved).  Usage: bash tools/gpu_quadearly.sh TAG
+# (build the variant first, on the CPU side: cd tinypathtracer_amd && make -j8 OBJDIR=variants/qe/build
+#  OUT=variants/qe/libtpt.so EXTRA=-DTPT_QUAD_EARLY=0 variants/qe/libtpt.so -- since round 5's final build
+#  the early loads are the default, so the variant is now the "without" side)
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-r05qe}

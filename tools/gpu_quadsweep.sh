@@ -1,6 +1,7 @@
 #!/bin/bash
 # Four lanes per pixel: strong-scaled C2 at N = 2, 4, 8 (every rank's share emulated)
-# with 1 and 4 lanes, refill at N = 8, and a 5-wave build (variants/q5).
+# with 1 and 4 lanes, refill at N = 8, and a 5-wave build (variants/q5: make -j8 OBJDIR=variants/q5/build
+# OUT=variants/q5/libtpt.so EXTRA=-DTPT_TRACE_WAVES_QUAD=5 variants/q5/libtpt.so in tinypathtracer_amd/).
 # Usage: bash tools/gpu_quadsweep.sh TAG
 set -o pipefail
 export TMPDIR=/tmp
