@@ -118,7 +118,8 @@ typedef struct {
      * one after the other (-25 % measured).  A host application that issues its own
      * greatest-priority work on the device while tpt_render runs shares those queues. */
     int32_t pipe_sets, pipe_chunks;
-    /* Lanes per pixel: 0 = auto, 1, or 2 = pair mode (scenes with delta lights): a side
+    /* Lanes per pixel: 0 = auto (pair mode with delta lights or env IS, else 4 on launches
+     * of at most 327,680 pixels, else 1), 1, or 2 = pair mode (scenes with delta lights): a side
      * lane per pixel traces each bounce's shadow rays while the path lane goes on, so a
      * sample's serial chain pays one traversal per bounce; 4 = four
      * lanes run each pixel's path together and split every 4-wide node visit (child k on
