@@ -7,10 +7,18 @@ Workload (BASELINE.json configs[1]): input box.gltf (Cornell box), 1920x1080,
 copyToFB, inputs resident in HBM.  A "ray" is one traverseBVH call (primary,
 extension, direct probe, shadow), counted by the kernel.
 
-N GPUs: one process per GPU (torch.distributed.run).  Default (--scaling
-strong, the split north_star names): a step is ONE frame of the workload
-above, dealt to the N GPUs in interleaved 16-row pixel bands, and one gather
-of the framebuffer bands to rank 0 (RCCL over xGMI) inside the timed region.
+N GPUs: one process per GPU (torch.distributed.run).  `python bench.py --gpus
+N` starts the N ranks itself (a launcher parent that never touches the GPU
+runs torch.distributed.run and exits with its code); under an external
+launcher WORLD_SIZE must equal --gpus.  Default (--scaling strong, the split
+north_star names): a step is ONE frame of the workload above, dealt to the N
+GPUs in 16-row pixel bands, and one gather of the framebuffer bands to rank 0
+(RCCL over xGMI) inside the timed region.  The deal (--deal cost, default):
+an untimed probe frame dealt in interleaved bands records each band's trace
+cost (tpt_params.band_cost), one all-reduce shares the costs, and every rank
+computes the same cost-balanced deal (shard.cost_deal) for the warm-up and
+timed steps -- as a renderer deals frame n+1 by frame n's costs; --deal
+interleaved keeps band b -> rank b % N.
 value = the frame's rays / max-over-ranks step time.  The same run then also
 times weak scaling (key "weak"; --weak-extra 0 skips it): a step is a batch of
 N frames (seeds 42 .. 42+N-1; the reference re-seeds every frame,
@@ -65,7 +73,9 @@ B_INNER, B_WIDE, B_LEAF, B_HIT, B_PIX = 56, 112, 52, 108, 12
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); N > 1 without an external launcher starts them "
+                         "(torch.distributed.run); default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
@@ -78,6 +88,9 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong: one frame banded across the N ranks (gather); "
                          "weak: N frames per step, each banded across the N ranks (all-to-all)")
+    ap.add_argument("--deal", choices=["cost", "interleaved"], default="cost",
+                    help="N > 1 (or --emulate-ranks): cost = bands dealt by an untimed probe frame's measured band "
+                         "costs (shard.cost_deal); interleaved = band b -> rank b %% N")
     ap.add_argument("--weak-extra", type=int, default=1,
                     help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
     ap.add_argument("--fast-extra", type=int, default=1,
@@ -352,8 +365,28 @@ KEYS = ["traversals", "internal_visits", "wide_visits", "leaf_tests", "shade_hit
         "rng_init_ms", "resolve_ms", "trace_launches", "trace_kernel_ms", "local_rays", "tree_wait_ms"]
 
 
+def launch_ranks(n):
+    """--gpus N > 1 without an external launcher: run N ranks of this script under
+    torch.distributed.run (127.0.0.1, a free port) and return its exit code.  The
+    parent never initialises the GPU (it only starts a child process)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+    elif args.gpus is not None and args.gpus != int(env_world):
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (one rank per GPU)")
     import torch
     import torch.distributed as dist
 
@@ -397,21 +430,55 @@ def main():
     flags = args.flags | (T._lib.FLAG_ENV_IS if args.env_is else 0) | (T._lib.FLAG_WAVEFRONT if args.wavefront else 0)
     emulate = args.emulate_ranks if (args.emulate_ranks > 1 and world == 1) else 0
     ranks = emulate or world
+    if world > 1 and args.dist_backend == "nccl" and torch.cuda.device_count() < local_world:
+        raise SystemExit(f"bench.py: {local_world} local ranks but {torch.cuda.device_count()} visible GPUs "
+                         "(one rank per GPU; --dist-backend gloo rehearses several ranks on one GPU)")
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
+    def probe_costs():
+        """The cost deal's input: one untimed frame of the workload dealt in
+        interleaved bands, every band's measured trace cost (tpt_params.band_cost;
+        this process's bands, or every emulated rank's in turn), summed over the
+        ranks by one all-reduce so every rank holds all of them."""
+        costs = np.zeros(shard.n_bands(H, args.band_rows), np.float32)
+        for r in (range(emulate) if emulate else [rank]):
+            d_scene.build(asynchronous=bool(args.async_build))
+            pt.doTraceFrames(d_scene, scene.m_camera, [args.seed], None, args.spp, max_depth=args.depth,
+                             band=(args.band_rows, ranks, r), flags=flags, refill=args.refill,
+                             pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
+                             lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch, band_cost=costs)
+        if world > 1:
+            t = torch.from_numpy(costs.astype(np.float64)).to(f"cuda:{dev}" if on_dev else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            costs = t.cpu().numpy()
+        return costs
+
+    deal, deal_info = None, None
+    if ranks > 1 and args.deal == "cost" and not args.wavefront:
+        tp = time.perf_counter()
+        costs = probe_costs()
+        deal = shard.cost_deal(costs, ranks)
+        il = shard.deal_loads(costs, shard.interleaved_deal(H, args.band_rows, ranks))
+        cl = shard.deal_loads(costs, deal)
+        deal_info = {"kind": "cost", "probe_s": round(time.perf_counter() - tp, 3),
+                     "predicted_max_over_mean": {"interleaved": round(max(il) / (sum(il) / ranks), 4),
+                                                 "cost": round(max(cl) / (sum(cl) / ranks), 4)},
+                     "bands_per_rank": [len(d) for d in deal]}
+
     def measure(scaling, band_index, extra_flags=0):
         """Warm-up + K timed steps of one scaling mode with this process
-        rendering band `band_index` of `ranks`; returns (max-over-ranks
-        elapsed, summed stats over ranks, this rank's stats, build ms, the last
-        step's frame output)."""
+        rendering band `band_index` of `ranks` (its share of `deal`, or of the
+        interleaved deal); returns (max-over-ranks elapsed, summed stats over
+        ranks, this rank's stats, build ms, the last step's frame output)."""
         n_frames = ranks if scaling == "weak" else 1
         seeds = [args.seed + f for f in range(n_frames)]
         radiances = [torch.zeros((H, W, 3), dtype=torch.float32, device=f"cuda:{dev}") for _ in range(n_frames)]
         band = (args.band_rows, ranks, band_index)
+        band_list = deal[band_index] if deal is not None else None
         build_ms = []
 
         def step():
@@ -424,13 +491,13 @@ def main():
                                   flags=flags | extra_flags,
                                   refill=args.refill, pipe_sets=args.pipe_sets, pipe_chunks=args.pipe_chunks,
                                   lanes_per_pixel=args.lanes_per_pixel, leaf_batch=args.leaf_batch,
-                                  wf_slots=args.wf_slots, wf_refill=args.wf_refill)
+                                  wf_slots=args.wf_slots, wf_refill=args.wf_refill, band_list=band_list)
             if world == 1:
                 return st, radiances[0]
             src = radiances if on_dev else [r.cpu() for r in radiances]   # gloo: host tensors
             if scaling == "weak":
-                return st, shard.exchange_frames(src, H, args.band_rows, world, rank)
-            return st, shard.gather_frame(src[0], H, args.band_rows, world, rank)
+                return st, shard.exchange_frames(src, H, args.band_rows, world, rank, deal=deal)
+            return st, shard.gather_frame(src[0], H, args.band_rows, world, rank, deal=deal)
 
         for _ in range(args.warmup):
             step()
@@ -590,6 +657,8 @@ def main():
             "build_threads": build_threads,
             "async_build": int(args.async_build),
         }
+        if ranks > 1:
+            out["deal"] = deal_info or {"kind": "interleaved"}
         if per_rank_ms:
             out["per_rank_ms"] = per_rank_ms
             out["emulate_run_ms"] = run_ms

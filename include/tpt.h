@@ -104,7 +104,8 @@ typedef struct {
     int32_t max_depth;            /* DEPTH_TRACE (reference: 8), 1..64 */
     uint64_t seed;                /* curand_init seed (reference: time()) */
     /* Interleaved row bands for multi-GPU sharding: this call renders rows y
-     * with (y / band_rows) % band_count == band_index.  band_count 1 = all. */
+     * with (y / band_rows) % band_count == band_index.  band_count 1 = all.
+     * band_list (below) replaces this deal with an explicit one. */
     int32_t band_rows, band_count, band_index;
     int32_t spp_per_launch;       /* 0 = auto; chunks the spp loop over launches */
     int32_t flags;                /* TPT_FLAG_* */
@@ -119,8 +120,8 @@ typedef struct {
      * greatest-priority work on the device while tpt_render runs shares those queues. */
     int32_t pipe_sets, pipe_chunks;
     /* Lanes per pixel: 0 = auto (pair mode with delta lights or env IS, else 4 on launches
-     * of at most 327,680 pixels, else 1), 1, or 2 = pair mode (scenes with delta lights): a side
-     * lane per pixel traces each bounce's shadow rays while the path lane goes on, so a
+     * of at most tpt_stats.resident_lanes pixels -- 327,680 on MI355X -- else 1), 1, or
+     * 2 = pair mode (scenes with delta lights): a side lane per pixel traces each bounce's shadow rays while the path lane goes on, so a
      * sample's serial chain pays one traversal per bounce; 4 = four
      * lanes run each pixel's path together and split every 4-wide node visit (child k on
      * lane k, leaf children tested at once), a shorter serial chain at a quarter of the
@@ -135,6 +136,19 @@ typedef struct {
      * traversing lanes below which a trace wave runs its pass -- finished walks out, the next
      * queued rays in (0 = auto, 40).  Bit-identical for any values. */
     int32_t wf_slots, wf_refill;
+    /* Explicit band deal (nullable; a zero-initialised params keeps the interleaved one): this
+     * call renders global bands band_list[0 .. band_list_len), band b = rows [b * band_rows,
+     * (b + 1) * band_rows) clipped to the frame, strictly ascending; band_count and band_index
+     * are then ignored.  Any deal is bit-identical to one GPU: the RNG subsequence is the global
+     * pixel index (path_tracer.cu:39,320).  Host memory, read during the call. */
+    int32_t band_list_len;
+    const int32_t* band_list;
+    /* Nullable, host memory, ceil(height / band_rows) floats: for each band this call renders,
+     * band_cost[b] = the summed life in microseconds of the trace waves that rendered it (megakernel
+     * only; 0 under TPT_FLAG_WAVEFRONT); other entries are left as they are.  A deal of the next
+     * frame's bands balanced by these costs (tinypathtracer_amd.shard.cost_deal) evens out ranks
+     * whose interleaved shares hold the heavy rows. */
+    float* band_cost;
 } tpt_params;
 
 #define TPT_FLAG_NO_COUNTERS   0x1   /* skip visit counters (traversals still counted) */
@@ -185,6 +199,12 @@ typedef struct {
                                      inline test); traversals - local_rays = BVH traversals run */
     double tree_wait_ms;          /* host wall time this call waited for a tpt_scene_build_async's host
                                      traversal-tree build, after enqueueing the RNG initialisation */
+    uint64_t resident_lanes;      /* the device's resident trace lanes (hipDeviceProp_t CUs x 4 SIMDs x
+                                     the one-lane variant's waves per SIMD x 64; MI355X 327,680): launches of
+                                     at most this many pixels run four lanes per pixel (lanes_per_pixel 0),
+                                     below twice it the latency-oriented (drained) variants */
+    int32_t lanes_per_pixel;      /* the lane mode the trace launches ran: 1, 2 (pair) or 4 */
+    int32_t drained;              /* 1: the drained-launch rule applied (refill, leaf batch, DRAIN variants) */
 } tpt_stats;
 
 typedef struct tpt_scene tpt_scene;

@@ -15,6 +15,13 @@ SCENE_DIR = os.path.join(ROOT, "tests", "golden", "scenes")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
     config.addinivalue_line("markers", "slow: long-running")
+    # TPT_TEST_FORCE_FLAGS=<int>: run the whole suite through a render variant
+    # (e.g. 32 = TPT_FLAG_WAVEFRONT, tools/gpu_wfsuite.sh); the library's hook,
+    # not an environment read inside the product API
+    forced = os.environ.get("TPT_TEST_FORCE_FLAGS")
+    if forced:
+        import tinypathtracer_amd as T
+        T.test_force_flags = int(forced, 0)
 
 
 def scene_path(name):

@@ -39,3 +39,28 @@ def test_two_ranks_bit_exact(mode, scene, port):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == mode
     assert d.get("gather_verified") is True, d
+
+
+def test_bench_gpus_flag_starts_the_ranks():
+    """`python bench.py --gpus 2` with no external launcher starts the two ranks
+    itself (torch.distributed.run under a parent that never touches the GPU):
+    n_gpus 2, the cost deal from a probe frame, and the gathered frame verified
+    bit for bit.  A --gpus that disagrees with an external WORLD_SIZE fails."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--verify-gather", "--spp", "8", "--width", "256", "--height", "144", "--steps", "1", "--warmup", "0",
+           "--cpu-baseline", "0", "--weak-extra", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d.get("gather_verified") is True, d
+    assert d["deal"]["kind"] == "cost" and sum(d["deal"]["bands_per_rank"]) == 9, d["deal"]
+    env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r2 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                        cwd=ROOT, env=env2, capture_output=True, text=True, timeout=120)
+    assert r2.returncode != 0 and "WORLD_SIZE" in r2.stderr

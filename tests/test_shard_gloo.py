@@ -92,3 +92,71 @@ def test_gloo_frame_batch_all_to_all(tmp_path, world):
         full, _, _ = O.render(ps, W, H, SPP, 8, 42 + f, trig_mode=1)
         got = np.load(str(tmp_path / f"frame{f}.npy"))
         assert np.array_equal(got.view(np.uint32), full.view(np.uint32)), f
+
+
+def test_cost_deal_partitions_and_balances():
+    """shard.cost_deal: every band dealt exactly once, ascending per rank, at most
+    ceil(bands / world) bands per rank (no rank holds more pixels than the
+    interleaved deal's largest share), deterministic, and its most loaded rank
+    no heavier than the interleaved deal's (strictly lighter on skewed costs)."""
+    from tinypathtracer_amd import shard
+    rng = np.random.default_rng(7)
+    for nb, world in ((68, 8), (135, 8), (68, 4), (9, 2), (5, 8), (1, 3)):
+        costs = (rng.random(nb) ** 4 * 100.0).astype(np.float32)
+        costs[nb // 2: nb // 2 + 3] *= 20.0   # a few heavy rows in the middle, as on box and C5
+        d = shard.cost_deal(costs, world)
+        assert len(d) == world
+        assert sorted(b for r in d for b in r) == list(range(nb))
+        assert all(r == sorted(r) for r in d)
+        assert max(len(r) for r in d) <= -(-nb // world)
+        assert d == shard.cost_deal(costs, world)
+        inter = [list(range(r, nb, world)) for r in range(world)]
+        assert max(shard.deal_loads(costs, d)) <= max(shard.deal_loads(costs, inter)) + 1e-3
+        if nb >= 4 * world:
+            assert max(shard.deal_loads(costs, d)) < max(shard.deal_loads(costs, inter))
+    # the deal's rows partition the frame, and band_row_ids follows the deal
+    d = shard.cost_deal(rng.random(68), 8)
+    rows = np.concatenate([shard.band_row_ids(1080, 16, 8, r, d) for r in range(8)])
+    assert sorted(rows.tolist()) == list(range(1080))
+    assert shard.interleaved_deal(1080, 16, 8)[3] == list(range(3, 68, 8))
+
+
+def _worker_deal(rank, world, port, out_path, deal):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from tinypathtracer_amd import shard
+    ps = O.load_scene(os.path.join(ROOT, "tests", "golden", "scenes", "box.gltf"))
+    nb = shard.n_bands(H, BAND)
+    rad = np.zeros((H, W, 3), np.float32)
+    for b in deal[rank]:   # this rank's bands of the explicit deal, one oracle band render each
+        rb, _, _ = O.render(ps, W, H, SPP, 8, 42, trig_mode=1, band_rows=BAND, band_count=nb, band_index=b,
+                            threads=1)
+        rows = shard.band_row_ids(H, BAND, nb, b)
+        rad[rows] = rb[rows]
+    frame = shard.gather_frame(torch.from_numpy(rad), H, BAND, world, rank, deal=deal)
+    if rank == 0:
+        np.save(out_path, frame.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_cost_deal_gather_bit_identical(tmp_path, world):
+    """A non-interleaved deal (shard.cost_deal of skewed costs): each rank
+    renders its bands, gather_frame(deal=...) assembles rank 0's frame, bit for
+    bit the one-process frame."""
+    from tinypathtracer_amd import shard
+    nb = shard.n_bands(H, BAND)
+    costs = np.array([1.0, 9.0, 8.0, 1.0, 0.5][:nb] + [0.1] * max(0, nb - 5), np.float32)
+    deal = shard.cost_deal(costs, world)
+    assert deal != shard.interleaved_deal(H, BAND, world)
+    out = str(tmp_path / "frame.npy")
+    mp.start_processes(_worker_deal, args=(world, _free_port(), out, deal), nprocs=world, join=True,
+                       start_method="spawn")
+    from oracle import oracle as O
+    ps = O.load_scene(os.path.join(ROOT, "tests", "golden", "scenes", "box.gltf"))
+    full, _, _ = O.render(ps, W, H, SPP, 8, 42, trig_mode=1)
+    assert np.array_equal(np.load(out).view(np.uint32), full.view(np.uint32))

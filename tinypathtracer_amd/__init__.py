@@ -394,12 +394,17 @@ class PathTracer:
                 seed=None, max_depth: int = 8, radiance=None, band=(16, 1, 0), spp_per_launch: int = 0,
                 flags: int = 0, refill: int = 0, accumulate: bool = False, pipe_sets: int = 0,
                 pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0, wf_slots: int = 0,
-                wf_refill: int = 0):
+                wf_refill: int = 0, band_list=None, band_cost=None):
         """One frame (path_tracer.cu:491-554).  framebuffer/radiance: numpy (host)
         or torch CUDA tensors / raw device pointers (device, int).
         accumulate=True: progressive rendering (TPT_FLAG_ACCUMULATE) -- continue
         the previous call's samples of the same frame; with seed None the
-        previous seed is kept (the reference re-seeds from time() every frame)."""
+        previous seed is kept (the reference re-seeds from time() every frame).
+        band = (band_rows, band_count, band_index): the interleaved deal;
+        band_list: an explicit deal (ascending global band ids of band_rows
+        rows each; band_count/band_index ignored); band_cost: a float32 array of
+        ceil(H / band_rows) entries that receives the rendered bands' costs
+        (tpt_params.band_cost, shard.cost_deal)."""
         if not d_scene.built:
             d_scene.build()
         W, H = self.m_width, self.m_height
@@ -413,6 +418,7 @@ class PathTracer:
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seed, band[0], band[1], band[2], spp_per_launch,
                         flags | _forced_flags(), refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch, wf_slots,
                         wf_refill)
+        keep = _deal_params(p, H, band, band_list, band_cost)  # noqa: F841 (alive through the call)
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
         rad_p = _addr(radiance)
@@ -425,10 +431,11 @@ class PathTracer:
                       nSamplesPerPixel: int = 64, max_depth: int = 8, radiances=None, band=(16, 1, 0),
                       spp_per_launch: int = 0, flags: int = 0, refill: int = 0, accumulate: bool = False,
                       pipe_sets: int = 0, pipe_chunks: int = 0, lanes_per_pixel: int = 0, leaf_batch: int = 0,
-                      wf_slots: int = 0, wf_refill: int = 0):
+                      wf_slots: int = 0, wf_refill: int = 0, band_list=None, band_cost=None):
         """A batch of independent frames in one trace launch (tpt_render_frames):
         frame f is doTrace(..., seed=seeds[f]) bit for bit.  framebuffers /
-        radiances: None or one buffer (or None) per frame."""
+        radiances: None or one buffer (or None) per frame.  band / band_list /
+        band_cost as in doTrace."""
         if not d_scene.built:
             d_scene.build()
         seeds = [int(x) for x in seeds]
@@ -441,6 +448,7 @@ class PathTracer:
         p = _lib.Params(W, H, nSamplesPerPixel, max_depth, seeds[0], band[0], band[1], band[2], spp_per_launch,
                         flags | _forced_flags(), refill, pipe_sets, pipe_chunks, lanes_per_pixel, leaf_batch, wf_slots,
                         wf_refill)
+        keep = _deal_params(p, H, band, band_list, band_cost)  # noqa: F841
         st = _lib.Stats()
         env = self.envLight.handle if self.envLight is not None else None
 
@@ -472,12 +480,33 @@ class PathTracer:
         return Frame(fb, rad, stats)
 
 
+# Test hook: OR-ed into every render's flags, so a whole parity suite can run
+# through a variant.  Only tests/conftest.py sets it (from TPT_TEST_FORCE_FLAGS,
+# e.g. 32 = TPT_FLAG_WAVEFRONT); the library itself reads no environment.
+test_force_flags = 0
+
+
 def _forced_flags() -> int:
-    """Test knob: TPT_TEST_FORCE_FLAGS (an integer) is OR-ed into every render's
-    flags, so the whole parity suite can run through a variant, e.g.
-    TPT_TEST_FORCE_FLAGS=32 (TPT_FLAG_WAVEFRONT).  Unset in production."""
-    v = os.environ.get("TPT_TEST_FORCE_FLAGS")
-    return int(v, 0) if v else 0
+    return int(test_force_flags)
+
+
+def _deal_params(p, height, band, band_list, band_cost):
+    """Fill tpt_params' explicit deal / cost output; returns the ctypes buffers
+    that must stay alive through the call."""
+    keep = []
+    if band_list is not None:
+        arr = (C.c_int32 * max(len(band_list), 1))(*[int(b) for b in band_list])
+        p.band_list_len = len(band_list)
+        p.band_list = C.cast(arr, C.POINTER(C.c_int32))
+        keep.append(arr)
+    if band_cost is not None:
+        nb = (height + band[0] - 1) // band[0]
+        if not (isinstance(band_cost, np.ndarray) and band_cost.dtype == np.float32 and band_cost.size == nb
+                and band_cost.flags["C_CONTIGUOUS"]):
+            raise ValueError(f"band_cost: a contiguous float32 array of {nb} entries")
+        p.band_cost = band_cost.ctypes.data_as(C.POINTER(C.c_float))
+        keep.append(band_cost)
+    return keep
 
 
 def _addr(buf):

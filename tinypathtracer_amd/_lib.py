@@ -61,7 +61,8 @@ class Params(C.Structure):
                 ("band_index", C.c_int32), ("spp_per_launch", C.c_int32), ("flags", C.c_int32),
                 ("refill", C.c_int32), ("pipe_sets", C.c_int32), ("pipe_chunks", C.c_int32),
                 ("lanes_per_pixel", C.c_int32), ("leaf_batch", C.c_int32), ("wf_slots", C.c_int32),
-                ("wf_refill", C.c_int32)]
+                ("wf_refill", C.c_int32), ("band_list_len", C.c_int32), ("band_list", C.POINTER(C.c_int32)),
+                ("band_cost", C.POINTER(C.c_float))]
 
 
 class Stats(C.Structure):
@@ -70,7 +71,8 @@ class Stats(C.Structure):
                 ("rng_init_ms", C.c_double), ("trace_ms", C.c_double), ("resolve_ms", C.c_double),
                 ("total_ms", C.c_double), ("trace_launches", C.c_int32), ("pad", C.c_int32),
                 ("wide_visits", C.c_uint64), ("accumulated_spp", C.c_uint64), ("trace_kernel_ms", C.c_double),
-                ("local_rays", C.c_uint64), ("tree_wait_ms", C.c_double)]
+                ("local_rays", C.c_uint64), ("tree_wait_ms", C.c_double), ("resident_lanes", C.c_uint64),
+                ("lanes_per_pixel", C.c_int32), ("drained", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}

@@ -82,6 +82,10 @@ struct TraceArgs {
     // frame
     int32_t width, height;
     int32_t band_rows, band_count, band_index, band_height;   // band_height: rows in this band
+    const int32_t* band_list;            // nullable: local band k renders global band band_list[k] (explicit deal;
+                                         //   ascending, so only the last entry may be a partial band)
+    unsigned long long* band_cost;       // nullable: per global band, the summed life of the waves that rendered
+                                         //   it (s_memrealtime ticks, 100 MHz), for cost-balanced deals
     int32_t n_frames;                    // frames of the batch (grid z); frame f's state at f * planes * W*H
     int32_t max_depth;
     int32_t samples;                     // samples for this launch
@@ -136,13 +140,14 @@ struct ResolveArgs {
     uint8_t* bgra;                       // device, W*H*4 (nullable)
     int32_t width, height;
     int32_t band_rows, band_count, band_index, band_height;
+    const int32_t* band_list;            // as TraceArgs
     int32_t spp;
 };
 
 // rng.hip
 hipError_t launch_rng_init(const uint32_t* jumps, uint64_t seed, int32_t width, int32_t band_rows,
-                           int32_t band_count, int32_t band_index, int32_t band_height, int32_t height,
-                           uint32_t* rng, hipStream_t s);
+                           int32_t band_count, int32_t band_index, const int32_t* band_list, int32_t band_height,
+                           int32_t height, uint32_t* rng, hipStream_t s);
 hipError_t launch_rng_init_linear(const uint32_t* jumps, uint64_t seed, uint64_t first, uint32_t n,
                                   uint32_t* states_aos, hipStream_t s);
 
@@ -237,6 +242,7 @@ hipError_t launch_wavefront(WfArgs w, uint32_t* h_count, hipEvent_t ev[2], int32
 // trace.hip
 hipError_t launch_trace(const TraceArgs& a, hipStream_t s);
 bool trace_quad_fits(const TraceArgs& a);   // lanes_per_pixel 4: one-lane records, the quads' stacks fit in LDS
+int trace_waves_per_simd();                 // the one-lane variants' __launch_bounds__ waves per SIMD
 hipError_t launch_trace_ptr(const void* a, hipStream_t s);   // a: const TraceArgs*
 // lone-wave step latency probe (tpt_debug_step_latency), a: const TraceArgs*
 hipError_t launch_step_latency_ptr(const void* a, uint32_t n, const float* o, const float* d, int nodes_lds,

@@ -394,7 +394,18 @@ struct tpt_scene {
     // progressive accumulation (TPT_FLAG_ACCUMULATE): the frame the rng/accum state belongs to
     bool acc_valid = false;
     int acc_w = 0, acc_h = 0, acc_rows = 0, acc_count = 0, acc_index = 0;
+    std::vector<int32_t> acc_list;          // the explicit deal it was rendered with (empty: interleaved)
     uint64_t acc_spp = 0;
+    // explicit band deals (tpt_params.band_list): the call's list, then each band
+    // set's share of it (host copy kept until the call's copies have run)
+    DevBuf<int32_t> band_lists;
+    std::vector<int32_t> band_lists_h;
+    DevBuf<unsigned long long> band_cost;   // per global band: summed wave life (tpt_params.band_cost)
+    std::vector<unsigned long long> band_cost_h;
+    // the chip, from hipDeviceProp_t: compute units, and the lanes the one-lane
+    // trace variant keeps resident (CUs x 4 SIMDs x its waves per SIMD x 64)
+    int32_t n_cu = 0;
+    uint64_t resident_lanes = 0;
     std::vector<uint64_t> acc_seeds;        // one per frame of the batch
     // overlapped launch pipeline: extra streams (set k >= 1 of a frame's rows)
     // and a pool of per-launch timing events
@@ -526,6 +537,15 @@ tpt_status tpt_scene_create(const tpt_scene_desc* d_in, int device, tpt_scene** 
     hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
     for (int i = 0; e == hipSuccess && i < 4; ++i) e = hipEventCreate(&s->ev[i]);
     if (e != hipSuccess) return cleanup(fail(TPT_ERR_HIP, std::string("stream/event: ") + hipGetErrorString(e)));
+    {
+        // the launch rules that key on the chip's resident lanes (tpt_render_frames:
+        // four lanes per pixel, drained launches) take them from the device
+        hipDeviceProp_t prop{};
+        e = hipGetDeviceProperties(&prop, device);
+        if (e != hipSuccess) return cleanup(fail(TPT_ERR_HIP, std::string("device properties: ") + hipGetErrorString(e)));
+        s->n_cu = prop.multiProcessorCount;
+        s->resident_lanes = (uint64_t)std::max(s->n_cu, 1) * 4u * (uint64_t)tpt::trace_waves_per_simd() * 64u;
+    }
 
     s->n_faces = (int32_t)d->n_faces;
     s->n_vertices = (int32_t)d->n_vertices;
@@ -1189,21 +1209,41 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     if (p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth < 1 || p->max_depth > 64)
         return fail(TPT_ERR_INVALID_ARG, "bad frame parameters");
     if ((int64_t)p->width * p->height > (int64_t)1 << 30) return fail(TPT_ERR_INVALID_ARG, "frame too large");
-    const int band_count = p->band_count > 0 ? p->band_count : 1;
     const int band_rows = p->band_rows > 0 ? p->band_rows : 16;
-    if (p->band_index < 0 || p->band_index >= band_count) return fail(TPT_ERR_INVALID_ARG, "bad band index");
+    // an explicit deal (band_list) replaces the interleaved one (band_count, band_index)
+    const bool listed = p->band_list != nullptr;
+    const int band_count = listed ? 1 : (p->band_count > 0 ? p->band_count : 1);
+    const int band_index = listed ? 0 : p->band_index;
+    if (!listed && (p->band_index < 0 || p->band_index >= band_count))
+        return fail(TPT_ERR_INVALID_ARG, "bad band index");
     if (env && env->device != s->device) return fail(TPT_ERR_INVALID_ARG, "env lives on another device");
+    const int W = p->width, H = p->height;
+    const int n_bands = (H + band_rows - 1) / band_rows;
+    std::vector<int32_t> list;
+    if (listed) {
+        if (p->band_list_len < 0 || p->band_list_len > n_bands)
+            return fail(TPT_ERR_INVALID_ARG, "band_list_len: 0 .. ceil(height / band_rows)");
+        list.assign(p->band_list, p->band_list + p->band_list_len);
+        for (size_t i = 0; i < list.size(); ++i)
+            if (list[i] < 0 || list[i] >= n_bands || (i > 0 && list[i] <= list[i - 1]))
+                return fail(TPT_ERR_INVALID_ARG, "band_list: strictly ascending band ids below ceil(height / band_rows)");
+    }
+    auto rows_of = [&](const std::vector<int32_t>& l) {
+        int n = 0;
+        for (int32_t b : l) n += std::min(band_rows, H - b * band_rows);
+        return n;
+    };
     DeviceGuard g(s->device);
     hipStream_t st = s->stream;
-    const int W = p->width, H = p->height;
     const size_t npix = (size_t)W * (size_t)H;
     const size_t nf = (size_t)n_frames;
-    const int bh = band_height_of(H, band_rows, band_count, p->band_index);
+    const int bh = listed ? rows_of(list) : band_height_of(H, band_rows, band_count, band_index);
     const std::vector<uint64_t> fseeds(seeds, seeds + nf);
 
     const bool resume = (p->flags & TPT_FLAG_ACCUMULATE) && s->acc_valid && s->acc_w == W && s->acc_h == H &&
-                        s->acc_rows == band_rows && s->acc_count == band_count && s->acc_index == p->band_index &&
-                        s->acc_seeds == fseeds && s->rng.n == 6 * npix * nf && s->accum.n == 3 * npix * nf;
+                        s->acc_rows == band_rows && s->acc_count == band_count && s->acc_index == band_index &&
+                        s->acc_list == list && s->acc_seeds == fseeds && s->rng.n == 6 * npix * nf &&
+                        s->accum.n == 3 * npix * nf;
     s->acc_valid = false;   // re-armed once this call has completed
     // per-frame state planes, frame f at offset f * (6|3) * npix
     HIP_OR_FAIL(s->rng.alloc(6 * npix * nf));
@@ -1211,13 +1251,28 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     HIP_OR_FAIL(s->counters.alloc(32));
     if (!resume) HIP_OR_FAIL(hipMemsetAsync(s->accum.p, 0, 3 * npix * nf * sizeof(float), st));   // thrust::fill (:534)
     HIP_OR_FAIL(hipMemsetAsync(s->counters.p, 0, 32 * sizeof(unsigned long long), st));
+    // the explicit deal's list on the device: the whole list first, the band sets'
+    // shares after it (written once the launch plan is known)
+    const int32_t* d_list = nullptr;
+    if (listed && !list.empty()) {
+        s->band_lists_h.assign(2 * list.size(), 0);
+        std::copy(list.begin(), list.end(), s->band_lists_h.begin());
+        HIP_OR_FAIL(s->band_lists.alloc(std::max(s->band_lists.n, 2 * list.size())));
+        HIP_OR_FAIL(hipMemcpyAsync(s->band_lists.p, s->band_lists_h.data(), list.size() * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, st));
+        d_list = s->band_lists.p;
+    }
+    if (p->band_cost) {
+        HIP_OR_FAIL(s->band_cost.alloc(std::max<size_t>(s->band_cost.n, (size_t)n_bands)));
+        HIP_OR_FAIL(hipMemsetAsync(s->band_cost.p, 0, (size_t)n_bands * sizeof(unsigned long long), st));
+    }
 
     // setupRandSeed (:513), one seed per frame; a progressive call continues the persisted streams
     HIP_OR_FAIL(hipEventRecord(s->ev[0], st));
     if (bh > 0 && !resume)
         for (size_t f = 0; f < nf; ++f)
-            HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, fseeds[f], W, band_rows, band_count, p->band_index, bh, H,
-                                             s->rng.p + f * 6 * npix, st));
+            HIP_OR_FAIL(tpt::launch_rng_init(s->jumps.p, fseeds[f], W, band_rows, band_count, band_index, d_list, bh,
+                                             H, s->rng.p + f * 6 * npix, st));
     HIP_OR_FAIL(hipEventRecord(s->ev[1], st));
     // an asynchronous scene build's host half ran while the above was enqueued
     double tree_wait_ms = 0.0;
@@ -1236,12 +1291,14 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     a.height = H;
     a.band_rows = band_rows;
     a.band_count = band_count;
-    a.band_index = p->band_index;
+    a.band_index = band_index;
+    a.band_list = d_list;
+    a.band_cost = p->band_cost ? s->band_cost.p : nullptr;
     a.band_height = bh;
     a.n_frames = n_frames;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
-    if (p->flags & (TPT_FLAG_APPROX_CULL | TPT_FLAG_FAST)) {   // culls without the exactness guards (trace.hip "Culling")
+    if (p->flags & TPT_FLAG_APPROX_CULL) {   // culls without the exactness guards (trace.hip "Culling")
         a.cull_eps = 0.0f;
         a.n_sliver_groups = 0;
         a.graze = 0;
@@ -1266,30 +1323,33 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // of a quad runs the pixel's path, each 4-wide visit split over them -- the
     // one-lane kernel logic, so no delta lights, env IS or reference order, and the
     // quads' stacks in LDS.  Auto on launches with no more pixels than the chip's
-    // resident lanes (256 CUs x 4 SIMDs x 5 waves x 64 = 327,680), which are their
-    // heaviest tiles' serial chains: strong-scaled C2 at N = 8 (259 K pixels per
-    // GPU, slowest rank) 314 -> 250 ms; at N = 4 (518 K) four lanes lose (463 vs
-    // 328 ms: four times the waves), so the chip is the bound.
+    // resident lanes (s->resident_lanes, from the device: MI355X 256 CUs x 4 SIMDs x
+    // 5 waves x 64 = 327,680), which are their heaviest tiles' serial chains:
+    // strong-scaled C2 at N = 8 (259 K pixels per GPU, slowest rank) 314 -> 250 ms;
+    // at N = 4 (518 K) four lanes lose (463 vs 328 ms: four times the waves), so
+    // the chip is the bound.
     const double launch_pix = (double)W * (double)std::max(bh, 1) * (double)nf;
-    const bool quad_ok = p->lanes_per_pixel != 2 && s->n_lights == 0 && !a.env_is &&
+    const double resident = (double)s->resident_lanes;
+    // (the wavefront variant has no lane modes: tpt.h, lanes_per_pixel is not used there)
+    const bool wavefront = (p->flags & TPT_FLAG_WAVEFRONT) != 0;
+    const bool quad_ok = !wavefront && p->lanes_per_pixel != 2 && s->n_lights == 0 && !a.env_is &&
                          !(p->flags & TPT_FLAG_REF_ORDER) && tpt::trace_quad_fits(a);
-    if (p->lanes_per_pixel == 4 && !quad_ok)
+    if (p->lanes_per_pixel == 4 && !quad_ok && !wavefront)
         return fail(TPT_ERR_INVALID_ARG,
                     "lanes_per_pixel 4: scenes without delta lights, no env IS, ordered traversal, stacks in LDS");
-    a.quad = (p->lanes_per_pixel == 4 || (p->lanes_per_pixel == 0 && launch_pix <= 327680.0 && quad_ok)) ? 1 : 0;
+    a.quad = (p->lanes_per_pixel == 4 || (p->lanes_per_pixel == 0 && launch_pix <= resident && quad_ok)) ? 1 : 0;
     // the trace grid's y extent is (band row blocks) x frames: 8-row workgroups in
     // pair mode, 16 otherwise (launch_trace)
-    {
+    if (!wavefront) {
         const int wg_rows = (pair_kernel || a.quad) ? 8 : 16;
         if ((size_t)((bh + wg_rows - 1) / wg_rows) * nf > 65535)
             return fail(TPT_ERR_INVALID_ARG, "frame batch too large for one launch");
     }
     // A launch with fewer pixels than about twice the chip's resident lanes
-    // (256 CUs x 4 SIMDs x 5 waves x 64 = 327,680: strong-scaled frames, small
-    // images) is bound by its heaviest waves' chains, not by throughput: batch
-    // the shading passes harder (C2 rank 0 of 8: refill 24 318 ms, 4: 276 ms;
-    // rank 0 of 4: flat).
-    const bool drained = launch_pix < 2.0 * 327680.0;
+    // (s->resident_lanes; strong-scaled frames, small images) is bound by its
+    // heaviest waves' chains, not by throughput: batch the shading passes harder
+    // (C2 rank 0 of 8: refill 24 318 ms, 4: 276 ms; rank 0 of 4: flat).
+    const bool drained = launch_pix < 2.0 * resident;
     // Shallow trees (few triangles) make a traversal short against a shading
     // pass, so passes are batched harder there: tir (6 triangles) refill 16
     // 84.6 Grays/s vs 24 72.6-78.9; box (1,932) 16 = 24; C5 (131 K) 16 -3 %.
@@ -1393,9 +1453,10 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // per-wave dump (phase-profiling builds) / traversal mismatch log (cull-verification builds)
     dbg_path = std::getenv("TPT_DEBUG_WAVES");
 #endif
-    // one record per wave of the largest grid (pair mode: 16x8-pixel workgroups)
+    // one record per wave of the largest grid: 8x8-pixel workgroups (four lanes per
+    // pixel; pair mode 16x8, one lane 16x16), 4 waves each, 8 words per wave
     const size_t dbg_launch =
-        8ull * 4 * (size_t)((W + 15) / 16) * (size_t)((std::max(bh, 1) + 7) / 8) * nf;
+        8ull * 4 * (size_t)((W + 7) / 8) * (size_t)((std::max(bh, 1) + 7) / 8) * nf;
     dbg_words = dbg_launch * std::max<size_t>(plan.size(), 1);   // one region per launch
     if (dbg_path) {
         HIP_OR_FAIL(s->debug.alloc(dbg_words));
@@ -1411,10 +1472,27 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
             HIP_OR_FAIL(hipStreamWaitEvent(qs[k], s->pipe_ev[0], 0));
         }
     }
-    // set k renders bands band_index + k * band_count of the band_count * nset interleave
+    // set k renders bands band_index + k * band_count of the band_count * nset
+    // interleave; of an explicit deal, list entries k, k + nset, ... (ascending, so
+    // a partial last band stays last in its set)
     int set_bh[kMaxPipe] = {bh};
-    for (int k = 0; k < nset; ++k)
-        set_bh[k] = nset == 1 ? bh : band_height_of(H, band_rows, band_count * nset, p->band_index + k * band_count);
+    size_t set_off[kMaxPipe] = {0};
+    for (int k = 0; k < nset; ++k) {
+        if (nset == 1) break;
+        if (listed) {
+            std::vector<int32_t> sub;
+            for (size_t i = (size_t)k; i < list.size(); i += (size_t)nset) sub.push_back(list[i]);
+            set_bh[k] = rows_of(sub);
+            set_off[k] = list.size();   // after the whole list, then the shares of sets 0 .. k-1
+            for (int j = 0; j < k; ++j) set_off[k] += (list.size() + nset - 1 - j) / nset;
+            std::copy(sub.begin(), sub.end(), s->band_lists_h.begin() + set_off[k]);
+        } else {
+            set_bh[k] = band_height_of(H, band_rows, band_count * nset, band_index + k * band_count);
+        }
+    }
+    if (listed && nset > 1 && !list.empty())
+        HIP_OR_FAIL(hipMemcpyAsync(s->band_lists.p + list.size(), s->band_lists_h.data() + list.size(),
+                                   list.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
     // issue the sets' launches interleaved in time order (chunk starts), so no
     // stream's queue runs ahead of the others on the host side
     std::vector<size_t> order(plan.size());
@@ -1449,8 +1527,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         ak.samples = plan[j].samples;
         if (nset > 1) {
             ak.band_count = band_count * nset;
-            ak.band_index = p->band_index + k * band_count;
+            ak.band_index = band_index + k * band_count;
             ak.band_height = set_bh[k];
+            if (listed) ak.band_list = s->band_lists.p + set_off[k];
         }
 #ifdef TPT_VERIFY_CULL
         if (dbg_path) ak.debug_waves = s->debug.p;   // one log, counters[24] indexes it
@@ -1494,7 +1573,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         r.height = H;
         r.band_rows = band_rows;
         r.band_count = band_count;
-        r.band_index = p->band_index;
+        r.band_index = band_index;
+        r.band_list = d_list;
         r.band_height = bh;
         r.spp = (int)total_spp;
         if (radiance_out) {
@@ -1529,6 +1609,15 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     HIP_OR_FAIL(hipMemcpyAsync(cnt, s->counters.p, sizeof cnt, hipMemcpyDeviceToHost, st));
     HIP_OR_FAIL(hipStreamSynchronize(st));
     if (cnt[4] != 0) return fail(TPT_ERR_HIP, "traversal stack overflow (BVH deeper than sized)");
+    if (p->band_cost) {   // per band this call rendered: its waves' summed life, in microseconds
+        s->band_cost_h.resize((size_t)n_bands);
+        HIP_OR_FAIL(hipMemcpy(s->band_cost_h.data(), s->band_cost.p, (size_t)n_bands * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost));
+        for (int b = 0; b < n_bands; ++b) {
+            const bool mine = listed ? std::binary_search(list.begin(), list.end(), b) : b % band_count == band_index;
+            if (mine) p->band_cost[b] = (float)((double)s->band_cost_h[(size_t)b] / 100.0);   // 100-MHz ticks
+        }
+    }
     if (dbg_path) {
 #ifdef TPT_VERIFY_CULL
         const size_t dump_words = std::min<size_t>(dbg_words, 16 * std::min<unsigned long long>(cnt[24], 4096));
@@ -1570,6 +1659,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         (void)hipEventElapsedTime(&ms, s->ev[2], s->ev[3]);
         stats->resolve_ms = ms;
         stats->trace_launches = launches;
+        stats->resident_lanes = s->resident_lanes;
+        stats->lanes_per_pixel = a.quad ? 4 : (pair_kernel ? 2 : 1);
+        stats->drained = a.drained;
         stats->total_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
@@ -1580,7 +1672,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     s->acc_h = H;
     s->acc_rows = band_rows;
     s->acc_count = band_count;
-    s->acc_index = p->band_index;
+    s->acc_index = band_index;
+    s->acc_list = list;
     s->acc_seeds = fseeds;
     s->acc_spp = total_spp;
     return TPT_OK;

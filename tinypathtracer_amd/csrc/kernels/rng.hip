@@ -43,12 +43,15 @@ __device__ void xorwow_init_device(const uint32_t* __restrict__ jumps, uint64_t 
 
 __global__ __launch_bounds__(256) void k_rng_init(const uint32_t* __restrict__ jumps, uint64_t seed,
                                                   int32_t width, int32_t band_rows, int32_t band_count,
-                                                  int32_t band_index, int32_t band_height, int32_t height,
+                                                  int32_t band_index, const int32_t* __restrict__ band_list,
+                                                  int32_t band_height, int32_t height,
                                                   uint32_t* __restrict__ rng) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int ly = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= width || ly >= band_height) return;
-    const int y = ((ly / band_rows) * band_count + band_index) * band_rows + (ly % band_rows);
+    // (trace_dev.hpp band_row: the interleaved deal, or an explicit band list)
+    const int lb = ly / band_rows;
+    const int y = (band_list ? band_list[lb] : lb * band_count + band_index) * band_rows + (ly % band_rows);
     if (y >= height) return;
     const size_t npix = (size_t)width * (size_t)height;
     const size_t off = (size_t)x + (size_t)y * (size_t)width;
@@ -69,11 +72,11 @@ __global__ void k_rng_init_linear(const uint32_t* __restrict__ jumps, uint64_t s
 }
 
 hipError_t launch_rng_init(const uint32_t* jumps, uint64_t seed, int32_t width, int32_t band_rows,
-                           int32_t band_count, int32_t band_index, int32_t band_height, int32_t height,
-                           uint32_t* rng, hipStream_t s) {
+                           int32_t band_count, int32_t band_index, const int32_t* band_list, int32_t band_height,
+                           int32_t height, uint32_t* rng, hipStream_t s) {
     dim3 grid((width + 63) / 64, (band_height + 3) / 4);
     hipLaunchKernelGGL(k_rng_init, grid, dim3(256), 0, s, jumps, seed, width, band_rows, band_count, band_index,
-                       band_height, height, rng);
+                       band_list, band_height, height, rng);
     return hipGetLastError();
 }
 

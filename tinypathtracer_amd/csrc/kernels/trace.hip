@@ -146,8 +146,11 @@ void k_trace(TraceArgs a) {
     const int ly = PAIR   ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 3)
                    : QUAD ? (by / nfr) * 8 + (wave >> 1) * 4 + (pl >> 2)
                           : (by / nfr) * 16 + (wave >> 1) * 8 + (pl >> 3);
-    int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
+    int y = band_row(ly, a.band_rows, a.band_count, a.band_index, a.band_list);
     const bool pixel = x < a.width && ly < a.band_height && y < a.height;
+    // cost-balanced deals (tpt_params.band_cost): the wave's life in s_memrealtime
+    // ticks, charged to the global band of its first row (lane 0's)
+    const unsigned long long t_cost0 = a.band_cost ? wall_clock64() : 0ull;
     bool active = pixel && !side;   // owns the pixel's RNG stream and sums
     uint32_t c_trav = 0, c_inner = 0, c_wide = 0, c_leaf = 0, c_shade = 0, c_ovf = 0;
     uint32_t c_local = 0;   // rays resolved in the shading pass without a BVH traversal
@@ -194,7 +197,7 @@ void k_trace(TraceArgs a) {
     // (QUAD: one stack per quad in its four lanes' columns; the host keeps it all in LDS)
     LaneStack<StackT, QUAD> stk;
     stk.lds = (TPT_LDS StackT*)(slds + a.lds_stack_offset) +
-              ((TPT_STACK_PAIRED && sizeof(StackT) == 2) ? 2 * tid : (QUAD ? (tid & ~3) : tid));
+              (QUAD ? (tid & ~3) : ((TPT_STACK_PAIRED && sizeof(StackT) == 2) ? 2 * tid : tid));
     stk.nlds = a.stack_lds_slots;
     PathRecords<MAXD, PAIR ? 128 : 256> rec;
     rec.lds = (TPT_LDS float*)(slds + a.lds_rec_offset) + (PAIR ? wave * 32 + pl : tid);
@@ -628,7 +631,7 @@ void k_trace(TraceArgs a) {
                     const int wj = j >> 6, lj = j & 63;
                     const int px = (tx + 1) * 16 + (wj & 1) * 8 + (lj & 7);
                     const int ply = (by / nfr) * 16 + (wj >> 1) * 8 + (lj >> 3);
-                    const int py = band_row(ply, a.band_rows, a.band_count, a.band_index);
+                    const int py = band_row(ply, a.band_rows, a.band_count, a.band_index, a.band_list);
                     if (px < a.width && ply < a.band_height && py < a.height) {
                         x = px;
                         y = py;
@@ -884,6 +887,9 @@ void k_trace(TraceArgs a) {
         if (s_ovf) atomicAdd(&a.counters[4], s_ovf);
         atomicAdd(&a.counters[5], s_wide);
         atomicAdd(&a.counters[9], s_local);
+        if (a.band_cost && ly < a.band_height)
+            atomicAdd(&a.band_cost[band_of(ly / a.band_rows, a.band_count, a.band_index, a.band_list)],
+                      wall_clock64() - t_cost0);
 #ifdef TPT_PROFILE_PHASES
         atomicAdd(&a.counters[6], p_done);
         atomicAdd(&a.counters[7], p_trav);
@@ -922,7 +928,7 @@ __global__ void k_resolve(ResolveArgs a) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int ly = blockIdx.y;
     if (x >= a.width || ly >= a.band_height) return;
-    const int y = band_row(ly, a.band_rows, a.band_count, a.band_index);
+    const int y = band_row(ly, a.band_rows, a.band_count, a.band_index, a.band_list);
     if (y >= a.height) return;
     const size_t npix = (size_t)a.width * (size_t)a.height;
     const size_t off = (size_t)x + (size_t)y * (size_t)a.width;
@@ -1231,6 +1237,10 @@ static void use_tile_pool(TraceArgs& a, dim3& grid, size_t& lds) {
     a.lds_pool_offset = (int)((lds + 15) / 16 * 16);
     lds = (size_t)a.lds_pool_offset + 16;
 }
+
+// waves per SIMD the one-lane trace variants are built for (__launch_bounds__):
+// with the device's CU count, the resident lanes the host's launch rules use
+int trace_waves_per_simd() { return TPT_TRACE_WAVES; }
 
 bool trace_quad_fits(const TraceArgs& a_in) {
     TraceArgs a = a_in;

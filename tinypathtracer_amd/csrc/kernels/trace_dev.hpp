@@ -956,8 +956,15 @@ __device__ __forceinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w
     else return env_lookup_call(env, w, h, d);
 }
 
-__device__ __forceinline__ int band_row(int ly, int band_rows, int band_count, int band_index) {
-    return ((ly / band_rows) * band_count + band_index) * band_rows + (ly % band_rows);
+// Local row ly of this call's bands -> frame row.  Interleaved deal: local band
+// k is global band k * band_count + band_index; an explicit deal (band_list,
+// tpt_params.band_list) names local band k's global band.
+__device__ __forceinline__ int band_of(int lb, int band_count, int band_index, const int32_t* band_list) {
+    return band_list ? band_list[lb] : lb * band_count + band_index;
+}
+__device__ __forceinline__ int band_row(int ly, int band_rows, int band_count, int band_index,
+                                        const int32_t* band_list) {
+    return band_of(ly / band_rows, band_count, band_index, band_list) * band_rows + (ly % band_rows);
 }
 
 __device__ __forceinline__ unsigned long long wave_sum(uint32_t v) {

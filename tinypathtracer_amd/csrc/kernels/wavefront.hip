@@ -65,7 +65,7 @@ __device__ __forceinline__ bool wf_pixel(const TraceArgs& a, int c, int& x, int&
     const int wave = tid >> 6, lane = tid & 63;
     x = bx * 16 + (wave & 1) * 8 + (lane & 7);
     const int ly = (by / nfr) * 16 + (wave >> 1) * 8 + (lane >> 3);
-    y = band_row(ly, a.band_rows, a.band_count, a.band_index);
+    y = band_row(ly, a.band_rows, a.band_count, a.band_index, a.band_list);
     return x < a.width && ly < a.band_height && y < a.height;
 }
 

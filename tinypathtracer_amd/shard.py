@@ -1,9 +1,15 @@
 """Pixel-band sharding across GPUs (one process per GPU) + framebuffer gather.
 
-Rows are dealt in interleaved bands of `band_rows` (band b -> rank b % world)
-so miss-heavy and hit-heavy rows spread evenly.  The RNG subsequence is the
-global pixel index (path_tracer.cu:39, :320), so any partition renders the
-same pixels bit-identically to a single GPU.
+Rows are dealt in bands of `band_rows`.  The default deal interleaves them
+(band b -> rank b % world) so miss-heavy and hit-heavy rows spread evenly; a
+cost deal (cost_deal) balances the ranks by the bands' measured trace costs
+from a previous frame (tpt_params.band_cost), for frames whose heavy rows the
+interleave leaves on a few ranks.  The RNG subsequence is the global pixel
+index (path_tracer.cu:39, :320), so any partition renders the same pixels
+bit-identically to a single GPU.
+
+A deal is a list, per rank, of ascending global band ids (tpt_params.band_list);
+deal=None everywhere below means the interleaved one.
 
 Two exchanges (RCCL over xGMI on the GPU box, gloo in the CPU tests):
   * gather_frame: one frame split across the ranks (strong scaling) -> one
@@ -18,17 +24,88 @@ from __future__ import annotations
 import numpy as np
 
 
-def band_row_ids(height: int, band_rows: int, world: int, rank: int) -> np.ndarray:
+def n_bands(height: int, band_rows: int) -> int:
+    return (height + band_rows - 1) // band_rows
+
+
+def interleaved_deal(height: int, band_rows: int, world: int):
+    """The default deal as explicit lists: band b -> rank b % world."""
+    return [list(range(r, n_bands(height, band_rows), world)) for r in range(world)]
+
+
+def band_row_ids(height: int, band_rows: int, world: int, rank: int, deal=None) -> np.ndarray:
     """Global row indices (row 0 = bottom) rendered by `rank`."""
     y = np.arange(height)
-    return y[(y // band_rows) % world == rank]
+    if deal is None:
+        return y[(y // band_rows) % world == rank]
+    return y[np.isin(y // band_rows, np.asarray(deal[rank], dtype=np.int64))]
 
 
-def max_band_height(height: int, band_rows: int, world: int) -> int:
-    return max(len(band_row_ids(height, band_rows, world, r)) for r in range(world))
+def max_band_height(height: int, band_rows: int, world: int, deal=None) -> int:
+    return max(len(band_row_ids(height, band_rows, world, r, deal)) for r in range(world))
 
 
-def gather_frame(radiance, height: int, band_rows: int, world: int, rank: int, dist=None, group=None):
+def cost_deal(costs, world: int, max_iter: int = 2000):
+    """Bands -> ranks by their measured costs (one float per global band, e.g.
+    the summed wave life tpt_params.band_cost reports for the previous frame):
+    longest-processing-time first -- heaviest band to the least-loaded rank --
+    with every rank capped at ceil(bands / world) bands, so no rank holds more
+    pixels than the interleaved deal's largest share (the lane-mode rules of
+    tpt_render key on a launch's pixels); then pairwise swaps and moves that
+    lower the larger of the two ranks' loads while the most loaded rank
+    improves.  Deterministic (ties by band id, then rank id), so every rank
+    computes the same deal from the same costs.  Returns per rank the
+    ascending band ids."""
+    c = [float(v) for v in costs]
+    nb = len(c)
+    if world < 1:
+        raise ValueError("world >= 1")
+    cap = (nb + world - 1) // world
+    own = [[] for _ in range(world)]
+    load = [0.0] * world
+    for b in sorted(range(nb), key=lambda i: (-c[i], i)):
+        r = min((r for r in range(world) if len(own[r]) < cap), key=lambda r: (load[r], r))
+        own[r].append(b)
+        load[r] += c[b]
+    for _ in range(max_iter):
+        m = max(range(world), key=lambda r: (load[r], -r))
+        best = None   # (new max of the pair, band out, rank in, band back or -1)
+        for i in own[m]:
+            for r in range(world):
+                if r == m:
+                    continue
+                if len(own[r]) < cap:   # move band i to rank r
+                    pm = max(load[m] - c[i], load[r] + c[i])
+                    if pm < load[m] and (best is None or pm < best[0]):
+                        best = (pm, i, r, -1)
+                for j in own[r]:        # swap band i with rank r's band j
+                    d = c[i] - c[j]
+                    if d <= 0.0:
+                        continue
+                    pm = max(load[m] - d, load[r] + d)
+                    if pm < load[m] and (best is None or pm < best[0]):
+                        best = (pm, i, r, j)
+        if best is None:
+            break
+        _, i, r, j = best
+        own[m].remove(i)
+        own[r].append(i)
+        load[m] -= c[i]
+        load[r] += c[i]
+        if j >= 0:
+            own[r].remove(j)
+            own[m].append(j)
+            load[r] -= c[j]
+            load[m] += c[j]
+    return [sorted(o) for o in own]
+
+
+def deal_loads(costs, deal):
+    """Summed cost per rank of a deal (its predicted balance)."""
+    return [float(sum(costs[b] for b in d)) for d in deal]
+
+
+def gather_frame(radiance, height: int, band_rows: int, world: int, rank: int, dist=None, group=None, deal=None):
     """Gather every rank's band rows of `radiance` [H, W, C] (torch tensor) into
     rank 0.  Returns the assembled frame on rank 0, None elsewhere.
 
@@ -38,8 +115,8 @@ def gather_frame(radiance, height: int, band_rows: int, world: int, rank: int, d
 
     if dist is None:
         import torch.distributed as dist
-    rows = band_row_ids(height, band_rows, world, rank)
-    mh = max_band_height(height, band_rows, world)
+    rows = band_row_ids(height, band_rows, world, rank, deal)
+    mh = max_band_height(height, band_rows, world, deal)
     w, c = radiance.shape[1], radiance.shape[2]
     slab = radiance.new_zeros((mh, w, c))
     idx = torch.as_tensor(rows, device=radiance.device, dtype=torch.long)
@@ -51,7 +128,7 @@ def gather_frame(radiance, height: int, band_rows: int, world: int, rank: int, d
         dist.gather(slab, gather_list=slabs, dst=0, group=group)
         out = radiance.new_zeros(radiance.shape)
         for r in range(world):
-            rr = band_row_ids(height, band_rows, world, r)
+            rr = band_row_ids(height, band_rows, world, r, deal)
             ri = torch.as_tensor(rr, device=radiance.device, dtype=torch.long)
             out.index_copy_(0, ri, slabs[r][: len(rr)])
         return out
@@ -59,7 +136,8 @@ def gather_frame(radiance, height: int, band_rows: int, world: int, rank: int, d
     return None
 
 
-def exchange_frames(radiances, height: int, band_rows: int, world: int, rank: int, dist=None, group=None):
+def exchange_frames(radiances, height: int, band_rows: int, world: int, rank: int, dist=None, group=None,
+                    deal=None):
     """Weak-scaling exchange for a batch of `world` frames: rank r rendered its
     band rows of every frame f (radiances[f], [H, W, C] tensors); one
     all-to-all (RCCL over xGMI: every rank sends to every peer at once, one
@@ -76,8 +154,8 @@ def exchange_frames(radiances, height: int, band_rows: int, world: int, rank: in
         raise ValueError("exchange_frames: one frame per rank")
     if world == 1:
         return radiances[0]
-    rows = band_row_ids(height, band_rows, world, rank)
-    mh = max_band_height(height, band_rows, world)
+    rows = band_row_ids(height, band_rows, world, rank, deal)
+    mh = max_band_height(height, band_rows, world, deal)
     ref = radiances[0]
     w, c = ref.shape[1], ref.shape[2]
     idx = torch.as_tensor(rows, device=ref.device, dtype=torch.long)
@@ -88,7 +166,7 @@ def exchange_frames(radiances, height: int, band_rows: int, world: int, rank: in
     dist.all_to_all_single(recv, send, group=group)
     out = ref.new_zeros(ref.shape)
     for r in range(world):
-        rr = band_row_ids(height, band_rows, world, r)
+        rr = band_row_ids(height, band_rows, world, r, deal)
         ri = torch.as_tensor(rr, device=ref.device, dtype=torch.long)
         out.index_copy_(0, ri, recv[r, : len(rr)])
     return out
