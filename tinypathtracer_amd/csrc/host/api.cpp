@@ -1463,15 +1463,6 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         HIP_OR_FAIL(hipMemsetAsync(s->debug.p, 0, dbg_words * sizeof(unsigned long long), st));
     }
     HIP_OR_FAIL(s->ensure_launch_events(2 * plan.size()));
-    hipStream_t qs[kMaxPipe] = {st};
-    if (nset > 1) {
-        HIP_OR_FAIL(s->ensure_pipe(nset));
-        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[0], st));   // fork: RNG init and the sums' reset are done
-        for (int k = 0; k < nset; ++k) {
-            qs[k] = s->pipe[k];
-            HIP_OR_FAIL(hipStreamWaitEvent(qs[k], s->pipe_ev[0], 0));
-        }
-    }
     // set k renders bands band_index + k * band_count of the band_count * nset
     // interleave; of an explicit deal, list entries k, k + nset, ... (ascending, so
     // a partial last band stays last in its set)
@@ -1492,7 +1483,16 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     }
     if (listed && nset > 1 && !list.empty())
         HIP_OR_FAIL(hipMemcpyAsync(s->band_lists.p + list.size(), s->band_lists_h.data() + list.size(),
-                                   list.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+                                   list.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));   // (before the fork)
+    hipStream_t qs[kMaxPipe] = {st};
+    if (nset > 1) {
+        HIP_OR_FAIL(s->ensure_pipe(nset));
+        HIP_OR_FAIL(hipEventRecord(s->pipe_ev[0], st));   // fork: RNG init, the sums' reset, the sets' band lists are done
+        for (int k = 0; k < nset; ++k) {
+            qs[k] = s->pipe[k];
+            HIP_OR_FAIL(hipStreamWaitEvent(qs[k], s->pipe_ev[0], 0));
+        }
+    }
     // issue the sets' launches interleaved in time order (chunk starts), so no
     // stream's queue runs ahead of the others on the host side
     std::vector<size_t> order(plan.size());
