@@ -88,7 +88,7 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong: one frame banded across the N ranks (gather); "
                          "weak: N frames per step, each banded across the N ranks (all-to-all)")
-    ap.add_argument("--deal", choices=["cost", "interleaved"], default="cost",
+    ap.add_argument("--deal", choices=["cost", "cost-heavy-first", "interleaved"], default="cost",
                     help="N > 1 (or --emulate-ranks): cost = bands dealt by an untimed probe frame's measured band "
                          "costs (shard.cost_deal); interleaved = band b -> rank b %% N")
     ap.add_argument("--weak-extra", type=int, default=1,
@@ -458,13 +458,18 @@ def main():
         return costs
 
     deal, deal_info = None, None
-    if ranks > 1 and args.deal == "cost" and not args.wavefront:
+    if ranks > 1 and args.deal.startswith("cost") and not args.wavefront:
         tp = time.perf_counter()
         costs = probe_costs()
-        deal = shard.cost_deal(costs, ranks)
+        nbands = shard.n_bands(H, args.band_rows)
+        deal = shard.cost_deal(costs, ranks, order="heavy_first" if args.deal == "cost-heavy-first" else "ascending",
+                               short_band=nbands - 1 if H % args.band_rows else None)
         il = shard.deal_loads(costs, shard.interleaved_deal(H, args.band_rows, ranks))
         cl = shard.deal_loads(costs, deal)
-        deal_info = {"kind": "cost", "probe_s": round(time.perf_counter() - tp, 3),
+        deal_info = {"kind": args.deal, "probe_s": round(time.perf_counter() - tp, 3),
+                     "band_costs_ms": [round(float(v) / 1e3, 2) for v in costs],
+                     "predicted_rank_ms": {"interleaved": [round(v / 1e3, 1) for v in il],
+                                           "cost": [round(v / 1e3, 1) for v in cl]},
                      "predicted_max_over_mean": {"interleaved": round(max(il) / (sum(il) / ranks), 4),
                                                  "cost": round(max(cl) / (sum(cl) / ranks), 4)},
                      "bands_per_rank": [len(d) for d in deal]}

@@ -121,8 +121,8 @@ typedef struct {
     int32_t pipe_sets, pipe_chunks;
     /* Lanes per pixel: 0 = auto (pair mode with delta lights or env IS, else 4 on launches
      * of at most tpt_stats.resident_lanes pixels -- 327,680 on MI355X -- else 1), 1, or
-     * 2 = pair mode (scenes with delta lights): a side lane per pixel traces each bounce's shadow rays while the path lane goes on, so a
-     * sample's serial chain pays one traversal per bounce; 4 = four
+     * 2 = pair mode (scenes with delta lights): a side lane per pixel traces each bounce's
+     * shadow rays while the path lane goes on, so a sample's serial chain pays one traversal per bounce; 4 = four
      * lanes run each pixel's path together and split every 4-wide node visit (child k on
      * lane k, leaf children tested at once), a shorter serial chain at a quarter of the
      * pixels per wave (scenes without delta lights, no env IS, ordered traversal; DESIGN.md
@@ -138,9 +138,10 @@ typedef struct {
     int32_t wf_slots, wf_refill;
     /* Explicit band deal (nullable; a zero-initialised params keeps the interleaved one): this
      * call renders global bands band_list[0 .. band_list_len), band b = rows [b * band_rows,
-     * (b + 1) * band_rows) clipped to the frame, strictly ascending; band_count and band_index
-     * are then ignored.  Any deal is bit-identical to one GPU: the RNG subsequence is the global
-     * pixel index (path_tracer.cu:39,320).  Host memory, read during the call. */
+     * (b + 1) * band_rows) clipped to the frame; distinct ids, a short last band (height not a
+     * multiple of band_rows) last; workgroups are dispatched in list order.  band_count and
+     * band_index are then ignored.  Any deal is bit-identical to one GPU: the RNG subsequence
+     * is the global pixel index (path_tracer.cu:39,320).  Host memory, read during the call. */
     int32_t band_list_len;
     const int32_t* band_list;
     /* Nullable, host memory, ceil(height / band_rows) floats: for each band this call renders,

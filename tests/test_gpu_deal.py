@@ -22,10 +22,10 @@ def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def _skewed_deal(nb, world, seed=3):
+def _skewed_deal(nb, world, seed=3, order="ascending", short_band=None):
     rng = np.random.default_rng(seed)
     costs = rng.random(nb).astype(np.float32) ** 3
-    d = shard.cost_deal(costs, world)
+    d = shard.cost_deal(costs, world, order=order, short_band=short_band)
     assert d != shard.interleaved_deal(nb * 16, 16, world)
     return d
 
@@ -48,7 +48,10 @@ def test_explicit_deal_bit_identical(scene, W, H, spp, kw):
         st = pt.doTrace(d, s.m_camera, None, spp, seed=42, radiance=full)
         nb = shard.n_bands(H, 16)
         for world in (2, 3):
-            deal = _skewed_deal(nb, world)
+            # world 3: each rank's bands heaviest first (dispatch order = list order), a
+            # short last band last
+            deal = _skewed_deal(nb, world, order="ascending" if world == 2 else "heavy_first",
+                                short_band=nb - 1 if H % 16 else None)
             acc = np.zeros((H, W, 3), np.float32)
             rays = 0
             for r in range(world):
@@ -99,11 +102,13 @@ def test_band_list_refusals():
     d = s.copySceneToDevice(0).build()
     try:
         pt = T.PathTracer("", W, H, 0)
-        for bad in ([1, 0], [0, 0], [3], [-1]):
+        for bad in ([0, 0], [3], [-1], [2, 0]):   # duplicate, out of range, the short band not last
             with pytest.raises(T.TPTError):
                 pt.doTrace(d, s.m_camera, None, 2, seed=1, band_list=bad)
         with pytest.raises(ValueError):
             pt.doTrace(d, s.m_camera, None, 2, seed=1, band_cost=np.zeros(2, np.float32))
+        st = pt.doTrace(d, s.m_camera, None, 2, seed=1, band_list=[1, 0, 2])   # any order, short band last
+        assert st["pixels"] == W * H
         # an empty list renders nothing
         st = pt.doTrace(d, s.m_camera, None, 2, seed=1, band_list=[])
         assert st["pixels"] == 0 and st["traversals"] == 0

@@ -83,7 +83,7 @@ struct TraceArgs {
     int32_t width, height;
     int32_t band_rows, band_count, band_index, band_height;   // band_height: rows in this band
     const int32_t* band_list;            // nullable: local band k renders global band band_list[k] (explicit deal;
-                                         //   ascending, so only the last entry may be a partial band)
+                                         //   only the last entry may be a short band); dispatched in list order
     unsigned long long* band_cost;       // nullable: per global band, the summed life of the waves that rendered
                                          //   it (s_memrealtime ticks, 100 MHz), for cost-balanced deals
     int32_t n_frames;                    // frames of the batch (grid z); frame f's state at f * planes * W*H

@@ -1224,9 +1224,14 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         if (p->band_list_len < 0 || p->band_list_len > n_bands)
             return fail(TPT_ERR_INVALID_ARG, "band_list_len: 0 .. ceil(height / band_rows)");
         list.assign(p->band_list, p->band_list + p->band_list_len);
-        for (size_t i = 0; i < list.size(); ++i)
-            if (list[i] < 0 || list[i] >= n_bands || (i > 0 && list[i] <= list[i - 1]))
-                return fail(TPT_ERR_INVALID_ARG, "band_list: strictly ascending band ids below ceil(height / band_rows)");
+        std::vector<uint8_t> seen((size_t)n_bands, 0);
+        const bool partial = H % band_rows != 0;   // the last band is short: it must come last (kernels
+        for (size_t i = 0; i < list.size(); ++i) {  // map local row ly to list[ly / band_rows])
+            if (list[i] < 0 || list[i] >= n_bands || seen[(size_t)list[i]]++ ||
+                (partial && list[i] == n_bands - 1 && i + 1 != list.size()))
+                return fail(TPT_ERR_INVALID_ARG, "band_list: distinct band ids below ceil(height / band_rows), "
+                                                 "a short last band last");
+        }
     }
     auto rows_of = [&](const std::vector<int32_t>& l) {
         int n = 0;
@@ -1298,7 +1303,9 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     a.n_frames = n_frames;
     a.max_depth = p->max_depth;
     a.flags = p->flags;
-    if (p->flags & TPT_FLAG_APPROX_CULL) {   // culls without the exactness guards (trace.hip "Culling")
+    // culls without the exactness guards (trace.hip "Culling"); the tolerance mode too:
+    // its C5 band measures the same with the guards kept
+    if (p->flags & (TPT_FLAG_APPROX_CULL | TPT_FLAG_FAST)) {
         a.cull_eps = 0.0f;
         a.n_sliver_groups = 0;
         a.graze = 0;
@@ -1464,8 +1471,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     }
     HIP_OR_FAIL(s->ensure_launch_events(2 * plan.size()));
     // set k renders bands band_index + k * band_count of the band_count * nset
-    // interleave; of an explicit deal, list entries k, k + nset, ... (ascending, so
-    // a partial last band stays last in its set)
+    // interleave; of an explicit deal, list entries k, k + nset, ... (a short last
+    // band, last in the list, stays last in its set)
     int set_bh[kMaxPipe] = {bh};
     size_t set_off[kMaxPipe] = {0};
     for (int k = 0; k < nset; ++k) {
@@ -1614,7 +1621,8 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
         HIP_OR_FAIL(hipMemcpy(s->band_cost_h.data(), s->band_cost.p, (size_t)n_bands * sizeof(unsigned long long),
                               hipMemcpyDeviceToHost));
         for (int b = 0; b < n_bands; ++b) {
-            const bool mine = listed ? std::binary_search(list.begin(), list.end(), b) : b % band_count == band_index;
+            const bool mine = listed ? std::find(list.begin(), list.end(), b) != list.end()
+                                     : b % band_count == band_index;
             if (mine) p->band_cost[b] = (float)((double)s->band_cost_h[(size_t)b] / 100.0);   // 100-MHz ticks
         }
     }

@@ -45,7 +45,7 @@ def max_band_height(height: int, band_rows: int, world: int, deal=None) -> int:
     return max(len(band_row_ids(height, band_rows, world, r, deal)) for r in range(world))
 
 
-def cost_deal(costs, world: int, max_iter: int = 2000):
+def cost_deal(costs, world: int, max_iter: int = 2000, order: str = "ascending", short_band=None):
     """Bands -> ranks by their measured costs (one float per global band, e.g.
     the summed wave life tpt_params.band_cost reports for the previous frame):
     longest-processing-time first -- heaviest band to the least-loaded rank --
@@ -54,8 +54,11 @@ def cost_deal(costs, world: int, max_iter: int = 2000):
     tpt_render key on a launch's pixels); then pairwise swaps and moves that
     lower the larger of the two ranks' loads while the most loaded rank
     improves.  Deterministic (ties by band id, then rank id), so every rank
-    computes the same deal from the same costs.  Returns per rank the
-    ascending band ids."""
+    computes the same deal from the same costs.  Returns per rank its band ids:
+    ascending (order "ascending"), or heaviest first (order "heavy_first": the
+    rank's launches dispatch its costliest bands first, so they do not end the
+    frame); a short last band (short_band) stays last either way, as
+    tpt_params.band_list requires."""
     c = [float(v) for v in costs]
     nb = len(c)
     if world < 1:
@@ -97,7 +100,11 @@ def cost_deal(costs, world: int, max_iter: int = 2000):
             own[m].append(j)
             load[r] -= c[j]
             load[m] += c[j]
-    return [sorted(o) for o in own]
+    if order == "ascending":
+        return [sorted(o) for o in own]
+    if order != "heavy_first":
+        raise ValueError("order: ascending or heavy_first")
+    return [sorted(o, key=lambda b: (b == short_band, -c[b], b)) for o in own]
 
 
 def deal_loads(costs, deal):
