@@ -95,8 +95,9 @@ def parse():
                     help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
     ap.add_argument("--fast-extra", type=int, default=1,
                     help="1 GPU: also time the tolerance mode (TPT_FLAG_FAST: FMA contraction, hardware "
-                         "rcp/sqrt/sin/cos, no culling guards; images within SURVEY 8(d)'s tolerance, not bit-exact) "
-                         "and report it under the key 'tolerance_mode' beside the exact headline")
+                         "rcp/sqrt/sin/cos, no culling guards; not bit-exact: within SURVEY 8(d)'s tolerance at C2-C4, "
+                         "C5's full-spp band meets the mean only) and report it under the key 'tolerance_mode' "
+                         "beside the exact headline")
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="1-GPU rehearsal of an N-rank run: every rank's bands of an N-way split in turn, "
                          "the step = the slowest rank's")
@@ -587,8 +588,12 @@ def main():
         tolerance = {"value": round(ft["traversals"] / fe / 1e6, 2), "unit": "Mrays/s",
                      "ms_per_step": round(fe / args.steps * 1e3, 3), "flags": "TPT_FLAG_FAST",
                      "what": "tolerance mode: FMA contraction and FMA slab tests, hardware rcp/sqrt/sin/cos, no "
-                             "culling guards; images within SURVEY 8(d)'s per-channel tolerance of the reference "
-                             "(tests/test_gpu_tolerance.py, test_gpu_fullsize.py mode fast), not bit-exact",
+                             "culling guards; not bit-exact.  Within SURVEY 8(d)'s per-channel tolerance of the "
+                             "reference (mean |d| <= 1e-3, p99 <= 1e-2, >= 99.5 % within one 8-bit step) at every "
+                             "BASELINE config at 1-2 spp and on the full-spp bands of C2, C3, C3 + env IS and C4; "
+                             "C5's full-spp band (2048 spp) meets the mean only (p99 0.0128, 96.0 % within one "
+                             "step) -- tests/test_gpu_tolerance.py, test_gpu_fullsize.py mode fast",
+                     "meets_survey_tolerance": args.scene != "c5",
                      "vs_exact": None}
 
     if rank == 0:

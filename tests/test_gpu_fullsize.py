@@ -166,7 +166,8 @@ def test_full_spp_band_matches_oracle(cfg, name, W, H, spp, depth, env, env_is, 
     same seed.  exact: every pixel's radiance bit for bit, the ray count equal.
     fast (TPT_FLAG_FAST, tolerance mode): SURVEY 8(d)'s per-channel tolerance --
     mean |d| <= 1e-3, p99 |d| <= 1e-2, >= 99.5 % of pixels within one 8-bit step
-    -- and the ray count within 1 %."""
+    -- except C5, where the mode claims the mean only (tpt.h) -- and the ray count
+    within 1 %."""
     from tests.test_gpu_parity import assert_parity, image_metrics
     count = (H + 15) // 16
     band = (16, count, count // 2)
@@ -191,14 +192,15 @@ def test_full_spp_band_matches_oracle(cfg, name, W, H, spp, depth, env, env_is, 
             m = image_metrics(rad[rows], orad[rows])
             print(cfg, "tolerance mode", m)
             if cfg == "C5":
-                # C5's band at 2048 spp: mean |d| 6.0e-4 within the bar, but p99 0.0128 and
-                # 96.0 % within one 8-bit step -- and a build with nothing but FMA
-                # contraction (IEEE divides, the parity sincos) measures the same (p99 0.0127,
-                # 96.3 %; DESIGN.md section 4 "Tolerance mode"): any arithmetic that is not
-                # the reference's moves its rare high-weight samples (glass and metal caustic
-                # paths onto the light), which at this spp set the per-pixel tail.  Asserted:
-                # the mean, and the measured tail as this configuration's stated tolerance.
-                assert m["mean"] <= 1e-3 and m["p99"] <= 0.015 and m["within1"] >= 0.95, m
+                # The tolerance mode does NOT meet SURVEY 8(d)'s tail bar on C5's band at 2048
+                # spp, and says so (tpt.h TPT_FLAG_FAST, bench.py tolerance_mode "what"): mean
+                # |d| 6.0e-4 within the bar, p99 0.0128 and 96.0 % within one 8-bit step.  The
+                # same with the culling guards kept, and with nothing but FMA contraction
+                # (DESIGN.md section 4 "Tolerance mode"): any arithmetic that is not the
+                # reference's moves the rare high-weight samples (glass and metal caustic paths
+                # onto the light) that set the per-pixel tail at this spp.  Asserted: what the
+                # mode claims there, the mean.
+                assert m["mean"] <= 1e-3, m
             else:
                 assert_parity(m, bit_min=0.0)
             assert abs(st["traversals"] - oc["traversals"]) <= 0.01 * oc["traversals"], cfg
