@@ -33,6 +33,9 @@
 #ifndef TPT_PROBE_SHORTCUT
 #define TPT_PROBE_SHORTCUT 1   // no emissive triangle: resolve direct probes in the shading pass
 #endif
+#ifndef TPT_PACKED_SORT   // 4-wide visits with 16-bit node ids: children sorted by packed (entry, link) keys
+#define TPT_PACKED_SORT 1
+#endif
 #ifndef TPT_LEAF_KP
 #define TPT_LEAF_KP 24    // run the triangle branch once this many lanes hold a parked leaf (or a.leaf_kb are blocked)
 #endif
@@ -421,6 +424,47 @@ __device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q
     const bool h1 = (i1 >= 0) & (fmaxf(k1, hd) <= fminf(e1, hi));
     const bool h2 = (i2 >= 0) & (fmaxf(k2, hd) <= fminf(e2, hi));
     const bool h3 = (i3 >= 0) & (fmaxf(k3, hd) <= fminf(e3, hi));
+    const int m = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+    if constexpr (TPT_PACKED_SORT && sizeof(StackT) == 2 && !QS) {
+        // 16-bit node ids: one sort key per child, the clamped slab entry's top 16 bits
+        // (sign, exponent, 7 mantissa bits; >= Delta/2, so never a denormal) over the
+        // link's 16 bits, sorted as floats with one min and one max per comparator.
+        // Entries within 1/128 of each other, and the children holding the origin
+        // (entry < Delta/2), order by link instead -- the visit order only steers:
+        // the walk's hit is the least t, then the larger leaf position, whatever the
+        // order (Culling), so the frame is the same.
+        const float inf = __builtin_inff();
+        auto pk = [inf](bool h, float k, int i, float hd_) {
+            return h ? __uint_as_float((__float_as_uint(fmaxf(k, hd_)) & 0xffff0000u) | ((uint32_t)i & 0xffffu)) : inf;
+        };
+        float p0 = pk(h0, k0, i0, hd), p1 = pk(h1, k1, i1, hd), p2 = pk(h2, k2, i2, hd), p3 = pk(h3, k3, i3, hd);
+#define TPT_CXP(a, b)                    \
+    {                                    \
+        const float lo_ = fminf(a, b);   \
+        b = fmaxf(a, b);                 \
+        a = lo_;                         \
+    }
+        TPT_CXP(p0, p1)
+        TPT_CXP(p2, p3)
+        TPT_CXP(p0, p2)
+        TPT_CXP(p1, p3)
+        TPT_CXP(p1, p2)
+#undef TPT_CXP
+        const int np = m > 0 ? m - 1 : 0;
+        const uint32_t u0 = __float_as_uint(np == 3 ? p3 : (np == 2 ? p2 : p1)), u1 = __float_as_uint(np == 3 ? p2 : p1),
+                       u2 = __float_as_uint(p1);
+        if (sp + 3 <= stk.nlds) {   // (StackT)u: the low 16 bits, the link
+            stk.lds[stk.off(sp)] = (StackT)u0;
+            stk.lds[stk.off(sp + 1)] = (StackT)u1;
+            stk.lds[stk.off(sp + 2)] = (StackT)u2;
+        } else {
+            stk.put(sp, (int)(u0 & 0xffffu));
+            stk.put(sp + 1, (int)(u1 & 0xffffu));
+            stk.put(sp + 2, (int)(u2 & 0xffffu));
+        }
+        sp += np;
+        return m > 0 ? (int)(__float_as_uint(p0) & 0xffffu) : -1;   // -1 when no child was entered
+    }
     i0 &= kLinkMask;
     i1 &= kLinkMask;
     i2 &= kLinkMask;
@@ -434,7 +478,6 @@ __device__ __forceinline__ int inner_visit4_q(const Trav& r, float4 q0, float4 q
     i1 = h1 ? i1 : -1;
     i2 = h2 ? i2 : -1;
     i3 = h3 ? i3 : -1;
-    const int m = (int)h0 + (int)h1 + (int)h2 + (int)h3;
 #define TPT_CX(ka, ia, kb, ib)          \
     {                                   \
         const bool sw = kb < ka;        \
