@@ -991,23 +991,38 @@ __device__ __forceinline__ void light_sample(const DevLight* __restrict__ Ls, in
 
 // sampleEnvLights (:288-294): Vec2UV (env_light.cuh:72-78) + point/clamp fetch
 // (texture.cu:156-170) of the RGBA8 equirect, row 0 = bottom.
+// the texel indices of Vec2UV (env_light.cuh:72-78) through the double-precision
+// atan2 / acos (ptrig.hpp): the exact path, cold (near texel edges only)
+__device__ __forceinline__ int env_col_exact(float z, float x, int w) {
+    float u = patan2_fast(z, x) / (2.0f * kPi);
+    if (u < 0.0f) u += 1.0f;
+    const int ix = (int)floorf(u * (float)w);
+    return ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
+}
+__device__ __forceinline__ int env_row_exact(float y, int h) {
+    const float v = 1.0f - pacos_fast(fclamp(y, 1.0f, -1.0f)) / kPi;
+    const int iy = (int)floorf(v * (float)h);
+    return iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
+}
+// Out of line where the lookup itself is inlined (the env importance-sampling
+// variants): the double path's constants and temporaries then stay out of the
+// kernel's register allocation (IS pair variant: 28 -> 8 spilled VGPRs at 128;
+// the one-lane IS variants 12 -> 0).  COLD = false: inline (the out-of-line
+// env_lookup_call of the other variants).
+static __device__ __noinline__ int env_col_exact_call(float z, float x, int w) { return env_col_exact(z, x, w); }
+static __device__ __noinline__ int env_row_exact_call(float y, int h) { return env_row_exact(y, h); }
+#ifndef TPT_ENV_COLD_CALL
+#define TPT_ENV_COLD_CALL 1
+#endif
+template <bool COLD>
 __device__ __forceinline__ V3 env_lookup_inl(const uint32_t* __restrict__ env, int w, int h, V3 d) {
     // the texel indices from fp32 bounds (ptrig.hpp env_col_fast / env_row_fast:
     // the same indices as the double evaluation wherever they decide); the
     // double path only within ~1e-3 texel of an edge
     int ix = TPT_ENV_FAST ? env_col_fast(d.z, d.x, w) : -1;
     int iy = TPT_ENV_FAST ? env_row_fast(d.y, h) : -1;
-    if (ix < 0) {
-        float u = patan2_fast(d.z, d.x) / (2.0f * kPi);
-        if (u < 0.0f) u += 1.0f;
-        ix = (int)floorf(u * (float)w);
-        ix = ix < 0 ? 0 : (ix > w - 1 ? w - 1 : ix);
-    }
-    if (iy < 0) {
-        const float v = 1.0f - pacos_fast(fclamp(d.y, 1.0f, -1.0f)) / kPi;
-        iy = (int)floorf(v * (float)h);
-        iy = iy < 0 ? 0 : (iy > h - 1 ? h - 1 : iy);
-    }
+    if (ix < 0) ix = (COLD && TPT_ENV_COLD_CALL) ? env_col_exact_call(d.z, d.x, w) : env_col_exact(d.z, d.x, w);
+    if (iy < 0) iy = (COLD && TPT_ENV_COLD_CALL) ? env_row_exact_call(d.y, h) : env_row_exact(d.y, h);
     const uint32_t t = env[(size_t)iy * (size_t)w + (size_t)ix];
     return (1.0f / 255.0f) * v3((float)(t & 0xffu), (float)((t >> 8) & 0xffu), (float)((t >> 16) & 0xffu));
 }
@@ -1017,11 +1032,11 @@ __device__ __forceinline__ V3 env_lookup_inl(const uint32_t* __restrict__ env, i
 // variants inline it (and env_is_sample): C3 with IS +25 % -- the calls'
 // register saves went to scratch.
 static __device__ __noinline__ V3 env_lookup_call(const uint32_t* __restrict__ env, int w, int h, V3 d) {
-    return env_lookup_inl(env, w, h, d);
+    return env_lookup_inl<false>(env, w, h, d);
 }
 template <bool INLINE>
 __device__ __forceinline__ V3 env_lookup(const uint32_t* __restrict__ env, int w, int h, V3 d) {
-    if constexpr (INLINE || TPT_ENV_INLINE) return env_lookup_inl(env, w, h, d);
+    if constexpr (INLINE || TPT_ENV_INLINE) return env_lookup_inl<true>(env, w, h, d);
     else return env_lookup_call(env, w, h, d);
 }
 
