@@ -300,3 +300,69 @@ def test_probe_pretest_exact_near_emitter_boxes(scenes, name):
     h3, _, _ = d.trace_rays(org, dirs, mode=3)
     assert np.array_equal(h3 >= 0, emit_hit), int(((h3 >= 0) != emit_hit).sum())
     assert np.array_equal(h3[emit_hit], h0[emit_hit])
+
+
+def grazing_arrival_rays(d, s, n, seed):
+    """Rays the origin-face rule does NOT route to the uncull'd path, aimed to
+    ARRIVE at another face at a grazing angle -- the residual cases of DESIGN.md
+    section 4 ("Residual gap"): a target face G, a point on it (interior, edge or
+    vertex), a direction within 1e-8 .. 1e-2 of G's plane; the origin is the hit
+    point Q of the reversed ray on the face F behind (computed as the kernel
+    computes hit points), kept only when the ray leaves F at |cos| >= 2e-3.
+    Returns origins, directions, the origin faces and the sine to G's plane."""
+    rng = np.random.default_rng(seed)
+    wv, _ = d.read_world()
+    tri = s.indices.reshape(-1, 3)
+    nf = len(tri)
+    v0, v1, v2 = (wv[tri[:, k]].astype(np.float64) for k in range(3))
+    nrm = np.cross(v1 - v0, v2 - v0)
+    area = np.linalg.norm(nrm, axis=1)
+    nrm /= np.maximum(area, 1e-30)[:, None]
+    m = 3 * n
+    g = rng.choice(nf, m, p=area / area.sum())
+    b = rng.dirichlet([1.0, 1.0, 1.0], m)
+    kind = rng.integers(0, 3, m)
+    b[kind == 1, rng.integers(0, 3, (kind == 1).sum())] = 0.0   # an edge
+    vsel = rng.integers(0, 3, m)
+    b[kind == 2] = 0.0
+    b[kind == 2, vsel[kind == 2]] = 1.0                          # a vertex
+    b /= b.sum(1, keepdims=True)
+    p = (b[:, :1] * v0[g] + b[:, 1:2] * v1[g] + b[:, 2:] * v2[g]).astype(np.float32)
+    ng = nrm[g]
+    tang = rng.normal(size=(m, 3))
+    tang -= (tang * ng).sum(1, keepdims=True) * ng
+    tang /= np.maximum(np.linalg.norm(tang, axis=1, keepdims=True), 1e-30)
+    sin_a = 10.0 ** rng.uniform(-8, -2, m)
+    side = np.where(rng.uniform(size=m) < 0.5, -1.0, 1.0)
+    dirs = (tang * np.sqrt(1.0 - sin_a ** 2)[:, None] + (side * sin_a)[:, None] * ng).astype(np.float32)
+    hb, tb, _ = d.trace_rays(p, -dirs, mode=0)                  # the face behind
+    ok = (hb >= 0) & (hb != g)
+    q = (p[ok] + tb[ok][:, None] * (-dirs[ok])).astype(np.float32)   # its hit point
+    f = hb[ok]
+    dd = dirs[ok].astype(np.float64)
+    cos_f = np.abs((nrm[f] * dd).sum(1)) / np.linalg.norm(dd, axis=1)
+    keep = cos_f >= 2e-3
+    return q[keep][:n], dirs[ok][keep][:n], f[keep][:n].astype(np.int32), sin_a[ok][keep][:n]
+
+
+@pytest.mark.parametrize("name,n", [("box", 400_000), ("box2", 200_000), ("ball", 200_000), ("tir", 100_000),
+                                    ("square", 100_000), ("c5", 400_000)])
+def test_culled_traversal_exact_on_grazing_arrivals(scenes, name, n):
+    """The residual cases the grazing rules do not route by construction
+    (DESIGN.md section 4): rays that leave their face at a normal angle and
+    arrive at another face within 1e-8 .. 1e-2 of its plane -- the reference's
+    hit there is an ill-conditioned Moller-Trumbore t, so a culled walk could
+    miss it, return a farther hit instead, or (shadow rays, probes) miss it as
+    an occluder.  Closest hit, any hit and the two-pass probe all equal the
+    reference order on every ray (the grazing-hit rule re-traces a grazing hit
+    the culled walk finds; the entry-cull margins keep the ones it must find)."""
+    s, d = scenes[name]
+    o, dirs, ofid, sin_a = grazing_arrival_rays(d, s, n, seed=17 + sum(map(ord, name)))
+    assert len(o) > n // 4, len(o)
+    h0, t0, uv0 = d.trace_rays(o, dirs, mode=0)
+    assert (h0 >= 0).mean() > 0.5
+    h1, t1, uv1 = d.trace_rays(o, dirs, mode=1, origin_fid=ofid)
+    bad = np.nonzero((h0 != h1) | (_bits(t0) != _bits(t1)) | (_bits(uv0) != _bits(uv1)).any(1))[0]
+    assert len(bad) == 0, (len(bad), len(o), [(int(i), int(h0[i]), int(h1[i]), float(t0[i]), float(t1[i]),
+                                                float(sin_a[i])) for i in bad[:8]])
+    _check_modes(s, d, o, dirs, h0, t0, uv0, ofid)
