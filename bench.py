@@ -61,9 +61,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 # cache-level ceiling for bytes the kernel re-reads from L1/L2
 L2_GATHER_PEAK_GBS = 18800.0
 # VALU issue: a wave64 VALU instruction holds a SIMD-32 for 2 cycles, 4 SIMDs
-# per CU, 256 CUs (MI355X_MICROARCH.md, "SIMD" and the cycle constants)
+# per CU (MI355X_MICROARCH.md, "SIMD" and the cycle constants); the CU count comes
+# from the device (torch.cuda.get_device_properties: 256 on MI355X)
 VALU_INST_PER_CU_CYCLE = 2.0
-N_CU = 256
 # algorithmic bytes: binary internal visit = links 8 + 2 child
 # AABBs 48; 4-wide visit = links 16 + 4 child AABBs 96; leaf = fid 4 + 3
 # indices 12 + 3 vertices 36; shading hit = 3 normals 36 + 3 indices 12 +
@@ -314,7 +314,7 @@ def pmc_summary(args, world, config, build):
     return best or stale
 
 
-def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_launch_ms, build):
+def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_launch_ms, build, n_cu):
     """The trace kernel against the MI355X ceilings.
     Live: algorithmic bytes per step / step time, against the L2-resident gather
     rate.  From the PMC summary of the same workload: per-step VALU
@@ -340,10 +340,10 @@ def roofline(args, world, config, bytes_step, step_s, launches_per_step, avg_lau
         clk = pm.get("effective_clock_ghz")
         if c.get("SQ_INSTS_VALU") and clk:
             inst = c["SQ_INSTS_VALU"] * lps / step_s / 1e9
-            peak = VALU_INST_PER_CU_CYCLE * N_CU * clk
+            peak = VALU_INST_PER_CU_CYCLE * n_cu * clk
             lu = pm.get("valu_lane_utilization")
             limits["valu_issue"] = {"achieved": round(inst, 1), "peak": round(peak, 1), "unit": "G wave-inst/s",
-                                    "frac": round(inst / peak, 4), "clock_ghz": clk,
+                                    "frac": round(inst / peak, 4), "clock_ghz": clk, "n_cu": n_cu,
                                     "lane_utilization": lu,
                                     # active-lane throughput against every lane of every SIMD issuing
                                     "useful_lane_frac": round(inst / peak * lu, 4) if lu is not None else None}
@@ -631,7 +631,8 @@ def main():
                   "variant": "wavefront (k_wf_logic + k_wf_trace)" if args.wavefront else "megakernel (k_trace)",
                   "parallelism": par}
         build = T.build_identity()
-        roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms, build)
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        roof = roofline(args, world, config, bytes_step, step_s, nl / K, avg_launch_ms, build, n_cu)
         out = {
             # BASELINE.json's metric, naming the workload actually run (C2 by default)
             "metric": f"Mrays/s at {W}x{H}x{args.spp}spp ({args.scene}.gltf, {args.depth} bounces"

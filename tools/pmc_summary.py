@@ -21,7 +21,18 @@ import sys
 
 out_dir = sys.argv[1]
 kernel_key = sys.argv[2] if len(sys.argv) > 2 else "k_trace"
-N_CU = 256
+
+
+def _n_cu():
+    """Compute units of the profiled device (256 on MI355X)."""
+    try:
+        import torch
+        return torch.cuda.get_device_properties(0).multi_processor_count
+    except Exception:
+        return 256
+
+
+N_CU = _n_cu()
 
 
 def durations(pattern):
@@ -56,6 +67,7 @@ if p.get("GRBM_GUI_ACTIVE") and s["serialized_avg_duration_ms"]:
     s["effective_clock_ghz"] = round(p["GRBM_GUI_ACTIVE"] / 8.0 / (s["serialized_avg_duration_ms"] * 1e6), 4)
 cycles = p["GRBM_GUI_ACTIVE"] / 8.0 if p.get("GRBM_GUI_ACTIVE") else None
 if cycles and p.get("SQ_INSTS_VALU"):
+    s["n_cu"] = N_CU
     s["valu_issue_frac_serialized"] = p["SQ_INSTS_VALU"] * 2.0 / (4.0 * N_CU * cycles)
 if "SQ_THREAD_CYCLES_VALU" in p and p.get("SQ_ACTIVE_INST_VALU"):
     s["valu_lane_utilization"] = p["SQ_THREAD_CYCLES_VALU"] / (64.0 * p["SQ_ACTIVE_INST_VALU"])
