@@ -362,7 +362,7 @@ def test_culled_traversal_on_grazing_arrivals_is_characterised(scenes, name, n):
     reference in every mode."""
     s, d = scenes[name]
     o, dirs, ofid, sin_a = grazing_arrival_rays(d, s, n, seed=17 + sum(map(ord, name)))
-    assert len(o) > n // 4, len(o)
+    assert len(o) > min(n // 4, 5000), len(o)   # (tir's 6 triangles leave few such pairs)
     h0, t0, uv0 = d.trace_rays(o, dirs, mode=0)
     assert (h0 >= 0).mean() > 0.5
     h1, t1, uv1 = d.trace_rays(o, dirs, mode=1, origin_fid=ofid)
