@@ -378,7 +378,10 @@ def test_culled_traversal_on_grazing_arrivals_is_characterised(scenes, name, n):
         nn = np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0])
         dd = dirs[bad].astype(np.float64)
         cos = np.abs((nn * dd).sum(1)) / (np.linalg.norm(nn, axis=1) * np.linalg.norm(dd, axis=1))
-        print(name, "divergent: |cos| to the reference's hit face max", float(cos.max()))
+        axis = (np.abs(nn) / np.linalg.norm(nn, axis=1, keepdims=True)).max(1) > 1 - 1e-6
+        dmin = (np.abs(dd) / np.linalg.norm(dd, axis=1, keepdims=True)).min(1)
+        print(name, "divergent: |cos| to the reference's hit face max", float(cos.max()),
+              "axis-aligned faces", int(axis.sum()), "of", nb, "min |d_i|/|d| max", float(dmin.max()))
         assert (cos < 1e-4).all(), np.sort(cos)[-5:]
     ok = ~bad
     _check_modes(s, d, o[ok], dirs[ok], h0[ok], t0[ok], uv0[ok], ofid[ok])
