@@ -459,7 +459,8 @@ def main():
         return costs
 
     deal, deal_info = None, None
-    if ranks > 1 and args.deal.startswith("cost") and not args.wavefront:
+    # (at N = 1, --deal cost-heavy-first orders the frame's own bands heaviest first)
+    if ((ranks > 1 and args.deal.startswith("cost")) or args.deal == "cost-heavy-first") and not args.wavefront:
         tp = time.perf_counter()
         costs = probe_costs()
         nbands = shard.n_bands(H, args.band_rows)
@@ -668,7 +669,7 @@ def main():
             "build_threads": build_threads,
             "async_build": int(args.async_build),
         }
-        if ranks > 1:
+        if ranks > 1 or deal_info:
             out["deal"] = deal_info or {"kind": "interleaved"}
         if per_rank_ms:
             out["per_rank_ms"] = per_rank_ms
