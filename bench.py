@@ -13,12 +13,13 @@ runs torch.distributed.run and exits with its code); under an external
 launcher WORLD_SIZE must equal --gpus.  Default (--scaling strong, the split
 north_star names): a step is ONE frame of the workload above, dealt to the N
 GPUs in 16-row pixel bands, and one gather of the framebuffer bands to rank 0
-(RCCL over xGMI) inside the timed region.  The deal (--deal cost, default):
-an untimed probe frame dealt in interleaved bands records each band's trace
-cost (tpt_params.band_cost), one all-reduce shares the costs, and every rank
-computes the same cost-balanced deal (shard.cost_deal) for the warm-up and
-timed steps -- as a renderer deals frame n+1 by frame n's costs; --deal
-interleaved keeps band b -> rank b % N.
+(RCCL over xGMI) inside the timed region.  The deal: band b -> rank b % N
+(default), or --deal cost: an untimed probe frame dealt in interleaved bands
+records each band's trace cost (tpt_params.band_cost), one all-reduce shares
+the costs, and every rank computes the same cost-balanced deal
+(shard.cost_deal) for the warm-up and timed steps -- as a renderer deals frame
+n+1 by frame n's costs (measured no better than the interleave, DESIGN.md
+section 6).
 value = the frame's rays / max-over-ranks step time.  The same run then also
 times weak scaling (key "weak"; --weak-extra 0 skips it): a step is a batch of
 N frames (seeds 42 .. 42+N-1; the reference re-seeds every frame,
@@ -88,9 +89,11 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong: one frame banded across the N ranks (gather); "
                          "weak: N frames per step, each banded across the N ranks (all-to-all)")
-    ap.add_argument("--deal", choices=["cost", "cost-heavy-first", "interleaved"], default="cost",
-                    help="N > 1 (or --emulate-ranks): cost = bands dealt by an untimed probe frame's measured band "
-                         "costs (shard.cost_deal); interleaved = band b -> rank b %% N")
+    ap.add_argument("--deal", choices=["interleaved", "cost", "cost-heavy-first"], default="interleaved",
+                    help="N > 1 (or --emulate-ranks): interleaved = band b -> rank b %% N (default); cost = bands "
+                         "dealt by an untimed probe frame's measured band costs (shard.cost_deal; measured no better, "
+                         "DESIGN.md section 6 'Band deals'); cost-heavy-first = the same, each rank's costliest "
+                         "bands dispatched first")
     ap.add_argument("--weak-extra", type=int, default=1,
                     help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
     ap.add_argument("--fast-extra", type=int, default=1,

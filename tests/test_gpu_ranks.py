@@ -52,7 +52,7 @@ def test_bench_gpus_flag_starts_the_ranks():
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--verify-gather", "--spp", "8", "--width", "256", "--height", "144", "--steps", "1", "--warmup", "0",
-           "--cpu-baseline", "0", "--weak-extra", "0"]
+           "--cpu-baseline", "0", "--weak-extra", "0", "--deal", "cost"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
