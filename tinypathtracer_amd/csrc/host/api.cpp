@@ -1385,12 +1385,14 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // largest run length <= 10 that divides a row's tiles per XCD (C5 3840 px:
     // 10 +4.1 %, 30 +3.7 %, 5 +2.1 %, 3 +1.9 %).
     a.xcd_run = 0;
+#ifndef TPT_XCD_RUNS_OFF   // (A/B builds: round-robin workgroups on every scene)
     if (s->n_faces > 16384) {
         const int gx = (W + 15) / 16, per = gx / 8;
         if (gx % 8 == 0)
             for (int g = std::min(per, 10); g >= 2 && a.xcd_run == 0; --g)
                 if (per % g == 0) a.xcd_run = g;
     }
+#endif
     a.rng = s->rng.p;
     a.accum = s->accum.p;
     a.counters = s->counters.p;
