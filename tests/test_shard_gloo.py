@@ -160,3 +160,14 @@ def test_gloo_cost_deal_gather_bit_identical(tmp_path, world):
     ps = O.load_scene(os.path.join(ROOT, "tests", "golden", "scenes", "box.gltf"))
     full, _, _ = O.render(ps, W, H, SPP, 8, 42, trig_mode=1)
     assert np.array_equal(np.load(out).view(np.uint32), full.view(np.uint32))
+
+
+def test_bench_refuses_gpus_that_disagree_with_world_size():
+    """bench.py under an external launcher: a --gpus that differs from WORLD_SIZE
+    exits non-zero before any GPU or torch work (so a driver that asks for N GPUs
+    never silently times one); runs on the CPU."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr, (r.returncode, r.stderr[-500:])
