@@ -36,6 +36,7 @@ def _skewed_deal(nb, world, seed=3, order="ascending", short_band=None):
     ("box", 256, 150, 16, {"pipe_sets": 3, "pipe_chunks": 2}),      # partial last band, three band sets
     ("ball", 256, 144, 16, {}),                                     # pair mode (delta light)
     ("tir", 200, 120, 32, {"lanes_per_pixel": 1, "pipe_sets": 2, "pipe_chunks": 4}),
+    ("box", 192, 112, 8, {"flags": 0x20}),                          # the wavefront variant (no band costs)
 ])
 def test_explicit_deal_bit_identical(scene, W, H, spp, kw):
     s = T.Scene(scene_path(scene))
@@ -61,7 +62,10 @@ def test_explicit_deal_bit_identical(scene, W, H, spp, kw):
                 rays += st_r["traversals"]
                 mine = np.zeros(nb, bool)
                 mine[deal[r]] = True
-                assert (cost[mine] > 0).all() and (cost[~mine] == 0).all(), (r, cost)
+                if kw.get("flags", 0) & T._lib.FLAG_WAVEFRONT:
+                    assert (cost == 0).all()   # (megakernel only, tpt.h)
+                else:
+                    assert (cost[mine] > 0).all() and (cost[~mine] == 0).all(), (r, cost)
                 assert st_r["pixels"] == W * len(shard.band_row_ids(H, 16, world, r, deal))
             assert int((_bits(acc) != _bits(full)).any(-1).sum()) == 0, (scene, world, kw)
             assert rays == st["traversals"]
@@ -148,5 +152,14 @@ def test_full_size_c2_cost_deal_8_ways():
         assert int((_bits(acc) != _bits(full)).any(-1).sum()) == 0
         assert rays == st["traversals"]
         assert st["resident_lanes"] > 0
+        # N = 2 (1 M pixels per rank: one lane per pixel, the full-occupancy variants, three
+        # band sets), each rank's bands heaviest first
+        deal2 = shard.cost_deal(costs, 2, order="heavy_first", short_band=nb - 1)
+        acc2 = np.zeros((H, W, 3), np.float32)
+        for r in range(2):
+            st_r = pt.doTrace(d, s.m_camera, None, spp, seed=42, max_depth=depth, radiance=acc2, band=(16, 2, r),
+                              band_list=deal2[r])
+            assert st_r["lanes_per_pixel"] == 1 and st_r["drained"] == 0
+        assert int((_bits(acc2) != _bits(full)).any(-1).sum()) == 0
     finally:
         d.close()
