@@ -346,17 +346,24 @@ void k_trace(TraceArgs a) {
 #ifdef TPT_PROFILE_PHASES
         if (__ballot(ts == TS_DONE) != 0ull) p_lp += (unsigned long long)__popcll(__ballot(ts == TS_DONE));
 #endif
-        if (ts == TS_DONE) {
+        // The shading pass, in two parts.  Pair mode exchanges the side lanes' finished
+        // direct sums between them (round 6), so a path lane whose side lane completes
+        // its level in this pass unwinds in this pass instead of waiting for the next.
+        const bool in_pass = ts == TS_DONE;
+        bool finish = false;   // the path ends this pass: unwind
+        bool begun = false;    // the next ray is already set up (inline probe pass 1)
+        bool redo = false;     // a grazing extension hit: traced again, uncull'd
+        bool shadow = false;   // the next ray is a shadow ray
+        bool tg = false;       // the next ray leaves its face within 1e-3 of its plane (grazing())
+        V3 L = v3(0.0f, 0.0f, 0.0f), td = rd;
+        if (in_pass) {
             TPT_SEC_BEGIN()
             // ---- consume the finished traversal (nothing yet for a fresh sample) ----
-            bool finish = false, lights_next = false, after = false;
+            bool lights_next = false, after = false;
             Hemi hb;              // this pass's hemisphere frame (new_direction), shared by the
             bool hb_ok = false;   // bounce's extension sample and its direct probe
-            bool begun = false;   // the next ray is already set up (inline probe pass 1)
-            V3 L = v3(0.0f, 0.0f, 0.0f);
             if (!LIGHTS) rd = r.d;   // the extension ray's direction (unused otherwise)
             Surf gpass = gsurf;   // the face this pass's new rays leave
-            bool redo = false;    // a grazing extension hit: traced again, uncull'd
             if (phase == PH_EXT) {
                 if (r.fid < 0) {   // miss: env radiance seeds the unwind (:358-362)
                     if (a.env) L = env_lookup<ENVIS>(a.env, a.env_w, a.env_h, rd);
@@ -417,9 +424,8 @@ void k_trace(TraceArgs a) {
                 finish = true;
             }
             TPT_SEC(1)
-            V3 td = rd;
-            bool shadow = false;
-            bool tg = redo;   // the next ray leaves its face within 1e-3 of its plane (grazing())
+            td = rd;
+            tg = redo;
             if (PAIR && lights_next && !side && li == 0 && pend < 0 && (a.n_lights > 0 || (ENVIS && env_pending))) {
                 // hand this bounce's shadow rays to the idle side lane (posted at the
                 // exchange below: origin r.o, material mk, level depth)
@@ -538,6 +544,33 @@ void k_trace(TraceArgs a) {
                 }
             }
             TPT_SEC(3)
+        }
+        bool woke = false;   // pair mode: a path lane that waited for its side lane, released mid-pass
+        if constexpr (PAIR) {
+            // ---- mid-pass exchange, side -> path: a level's direct sum, in light order ----
+            // (a side lane becomes ready in the first part of its pass; a path lane that
+            // finishes in this pass, or has waited since an earlier one, then unwinds in
+            // the second part -- the same sums in the same order, one pass sooner)
+            const int jready = __shfl_xor((int)ready, 1, 64);
+            const float dx = __shfl_xor(direct.x, 1, 64), dy = __shfl_xor(direct.y, 1, 64),
+                        dz = __shfl_xor(direct.z, 1, 64);
+            const int rl = __shfl_xor(jlevel, 1, 64);
+            if (!side && jready) {
+                rec.put(rl, 2, dx);
+                rec.put(rl, 3, dy);
+                rec.put(rl, 4, dz);
+                pend = -1;
+                if (!in_pass && phase == PH_WAIT) {   // its unwind seed waits in `direct`
+                    woke = true;
+                    ts = TS_DONE;
+                    L = direct;
+                    finish = true;
+                    td = rd;
+                }
+            }
+            ready = false;
+        }
+        if (in_pass || woke) {
             if (PAIR && finish && pend >= 0) {
                 // the side lane still sums a level's shadow rays: wait for it (exchange below)
                 direct = L;
