@@ -81,6 +81,13 @@ __device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int p
 }
 #endif
 
+// Pair mode's mid-pass exchange (round 6): 1 in every pair variant, 2 only with env
+// importance sampling, 0 off (the side lanes' sums then reach their path lanes at the
+// end of the pass only).
+#ifndef TPT_PAIR_MID
+#define TPT_PAIR_MID 1
+#endif
+
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
 // state (direct term, normal, light index, incoming direction -- r.d during an
 // extension ray) is dead across traversals and drops out of the registers.
@@ -546,7 +553,7 @@ void k_trace(TraceArgs a) {
             TPT_SEC(3)
         }
         bool woke = false;   // pair mode: a path lane that waited for its side lane, released mid-pass
-        if constexpr (PAIR) {
+        if constexpr (PAIR && (TPT_PAIR_MID == 1 || (TPT_PAIR_MID == 2 && ENVIS))) {
             // ---- mid-pass exchange, side -> path: a level's direct sum, in light order ----
             // (a side lane becomes ready in the first part of its pass; a path lane that
             // finishes in this pass, or has waited since an earlier one, then unwinds in
