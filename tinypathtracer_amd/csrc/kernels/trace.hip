@@ -85,7 +85,7 @@ __device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int p
 // importance sampling, 0 off (the side lanes' sums then reach their path lanes at the
 // end of the pass only).
 #ifndef TPT_PAIR_MID
-#define TPT_PAIR_MID 1
+#define TPT_PAIR_MID 2
 #endif
 
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
