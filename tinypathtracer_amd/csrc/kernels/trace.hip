@@ -88,6 +88,16 @@ __device__ __noinline__ void verify_ray(const TraceArgs& a, const Trav& r, int p
 #define TPT_PAIR_MID 2
 #endif
 
+// Shadow rays' first step in the pass (round 6): a fresh shadow ray (delta light or env
+// sample) takes its root visit before the wave enters the traversal loop; when no
+// child of the root passes, the ray is finished there, and the wave runs its shading
+// pass again before traversing, so a side lane's next shadow ray (or its direct sum)
+// follows at once instead of after the traversal round.  The same visit, the same
+// counters: the frame is the same.  1 on, 0 off.
+#ifndef TPT_SHADOW_FIRST
+#define TPT_SHADOW_FIRST 0
+#endif
+
 // LIGHTS == false (no delta lights, packed 2-word records): the shadow-ray
 // state (direct term, normal, light index, incoming direction -- r.d during an
 // extension ray) is dead across traversals and drops out of the registers.
@@ -799,6 +809,21 @@ void k_trace(TraceArgs a) {
             if (side && ts == TS_IDLE && pdead) ts = TS_DEAD;
         }
         if (__ballot(ts != TS_DEAD) == 0ull) break;
+        if constexpr (TPT_SHADOW_FIRST && ORDERED && (LIGHTS || ENVIS) && !QUAD) {
+            // a fresh shadow ray's root visit (the loop's first step for it, below)
+            bool quick = false;
+            if (ts == TS_TRAV && r.mode == TM_ANY && r.fin && r.node == 0 && r.sp == 0 && r.pend < 0 &&
+                r.fid < 0 && r.t == kRealMax) {
+                ++c_wide;
+                const int next = inner_visit4(r, a.inner4, snodes, a.lds_nodes, stk, r.sp);
+                r.node = next >= 0 ? next : (r.sp == 0 ? -1 : stk.get(--r.sp));
+                if (r.node < 0) {   // no child passes: the ray is done, unoccluded
+                    ts = TS_DONE;
+                    quick = true;
+                }
+            }
+            if (__ballot(quick) != 0ull) continue;   // shade those lanes before traversing
+        }
 #ifdef TPT_PROFILE_PHASES
         t_loop0 = wall_clock64();
         p_done += t_loop0 - t_iter0;

@@ -97,6 +97,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #ifndef TPT_SHARE_HEMI
 #define TPT_SHARE_HEMI 0   // 1: the direct probe reuses the extension sample's hemisphere frame (new_direction)
 #endif
+#ifndef TPT_FMA_SLAB_UB
+#define TPT_FMA_SLAB_UB 0   // 1: A/B builds only -- every slab as one FMA per bound (NOT exact: the
+                            // upper bound of the inner-box FMA cut, DESIGN.md section 5 "Round 6")
+#endif
 #ifndef TPT_ENV_INLINE
 #define TPT_ENV_INLINE 0   // 1: env_lookup inlined in every variant (A/B builds)
 #endif
@@ -310,7 +314,7 @@ __device__ __forceinline__ void inner_visit(const Trav& r, const float4* __restr
 // differ from the ternaries; only comparisons consume T0/T1.
 __device__ __forceinline__ void slab_minmax(const V3& o, const V3& inv, float nx, float ny, float nz, float xx,
                                             float xy, float xz, float& t0, float& t1) {
-#if TPT_FAST
+#if TPT_FAST || TPT_FMA_SLAB_UB
     // (n - o) / d as one FMA per bound: n * (1/d) - o * (1/d) (the o * (1/d) terms
     // are common to every box a visit tests)
     const float ox = -(o.x * inv.x), oy = -(o.y * inv.y), oz = -(o.z * inv.z);

@@ -86,7 +86,7 @@ def helper_ranges(src):
 def kernel_ranges(src):
     k = src.find(r"^void k_trace\(")
     loop_top = src.find(r"^    for \(;;\) \{", k)
-    done = src.find(r"if \(ts == TS_DONE\) \{", loop_top + 1)
+    done = src.find(r"if \(in_pass\) \{", loop_top + 1)
     s = [src.find(rf"TPT_SEC\({i}\)", done) for i in range(1, 7)]
     tl = src.find(r"const int thr = refill;", s[5])
     leafdec = src.find(r"const unsigned long long hb = __ballot\(has\);", tl)
