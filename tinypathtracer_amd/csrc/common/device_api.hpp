@@ -111,6 +111,7 @@ struct TraceArgs {
     int32_t drained;                     // 1: the launch cannot fill the chip (latency-oriented DRAIN variants)
     int32_t quad;                        // 1: four lanes per pixel, each node visit split over them (k_trace QUAD)
     int32_t xcd_run;                     // > 0: workgroup tiles dealt to XCDs in runs of this many (k_trace)
+    int32_t xcd_rot;                     // the runs' XCD rotation of this launch (its chunk of the set's spp)
     int32_t tile_pool;                   // 1: each workgroup renders two adjacent tiles, the second as a pixel
                                          //    pool its finished lanes draw from (k_trace; set by launch_trace)
     int32_t lds_pool_offset;             // set by launch_trace: byte offset of the pool counter in LDS

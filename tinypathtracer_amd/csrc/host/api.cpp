@@ -152,6 +152,9 @@ std::vector<uint32_t>& host_jumps() {
 
 constexpr int kMaxPipe = 4;         // overlapped launch sets per frame (GPU_MAX_HW_QUEUES is 4)
 constexpr int kPipeMinChunk = 128;  // spp per pipelined launch, at least
+#ifndef TPT_XCD_ROT
+#define TPT_XCD_ROT 1   // XCD runs rotate by one per chunk of a set (0: every chunk alike; A/B builds)
+#endif
 
 int band_height_of(int height, int band_rows, int band_count, int band_index) {
     int n = 0;
@@ -1385,6 +1388,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // largest run length <= 10 that divides a row's tiles per XCD (C5 3840 px:
     // 10 +4.1 %, 30 +3.7 %, 5 +2.1 %, 3 +1.9 %).
     a.xcd_run = 0;
+    a.xcd_rot = 0;
 #ifndef TPT_XCD_RUNS_OFF   // (A/B builds: round-robin workgroups on every scene)
     if (s->n_faces > 16384) {
         const int gx = (W + 15) / 16, per = gx / 8;
@@ -1528,12 +1532,17 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
                         std::string(#expr) + ": " + hipGetErrorString(e_));                                    \
         }                                                                                                      \
     } while (0)
+    int set_chunks[kMaxPipe] = {};   // launches issued per set so far (XCD run rotation)
     for (size_t oi = 0; oi < order.size(); ++oi) {
         const size_t j = order[oi];
         const int k = plan[j].set;
         if (set_bh[k] <= 0) continue;
         tpt::TraceArgs ak = a;
         ak.samples = plan[j].samples;
+        // XCD runs: chunk c of a set rotates the runs' XCDs by c (trace.hip prologue), so a
+        // set whose few rows leave the per-launch rotation incomplete still spreads its heavy
+        // columns over every XCD across its chunks
+        ak.xcd_rot = TPT_XCD_ROT ? (set_chunks[k]++ & 7) : 0;
         if (nset > 1) {
             ak.band_count = band_count * nset;
             ak.band_index = band_index + k * band_count;

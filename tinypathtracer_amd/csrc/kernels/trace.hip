@@ -138,9 +138,13 @@ void k_trace(TraceArgs a) {
     // XCD gets every column over the launch (a permutation of the row's tiles;
     // the host checks that xcd_run divides gridDim.x / 8).  C5 +4 %; on box,
     // whose scene is L2-resident anyway, runs cost 2-7 % (the heavy middle
-    // columns then load fewer XCDs), so it stays off there.
+    // columns then load fewer XCDs), so it stays off there.  A launch of few rows
+    // (a strong-scaled share: 6 rows of workgroups per set) does not complete the
+    // rotation, and its heavy columns would load the same XCDs in every chunk of
+    // the set's spp: the host rotates each chunk by one more (xcd_rot), so over 8
+    // chunks every XCD takes every tile once.
     if (a.xcd_run > 0) {
-        const int g = a.xcd_run, k = ((bx & 7) + by) & 7, m = bx >> 3;
+        const int g = a.xcd_run, k = ((bx & 7) + by + a.xcd_rot) & 7, m = bx >> 3;
         bx = ((m / g) * 8 + k) * g + m % g;
     }
     const int frame = by % nfr;
