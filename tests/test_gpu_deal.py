@@ -163,3 +163,29 @@ def test_full_size_c2_cost_deal_8_ways():
         assert int((_bits(acc2) != _bits(full)).any(-1).sum()) == 0
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("W,H,kw", [
+    (256, 96, {"pipe_sets": 2, "pipe_chunks": 4}),                       # XCD runs of 2 tiles, 4 rotations per set
+    (640, 80, {"pipe_sets": 3, "pipe_chunks": 8, "band": (16, 2, 1)}),    # runs of 5, a strong-scaled share
+])
+def test_xcd_runs_rotated_per_chunk_bit_identical(W, H, kw):
+    """A scene larger than an XCD's L2 (c5, 131 K triangles) deals tiles to XCDs in
+    runs that rotate by one per chunk of a set's samples (api.cpp xcd_rot): the
+    chunked, pipelined render equals one launch bit for bit."""
+    s = T.Scene(scene_path("c5"))
+    d = s.copySceneToDevice(0).build()
+    try:
+        pt = T.PathTracer("", W, H, 0)
+        spp = 16
+        band = kw.pop("band", (16, 1, 0))
+        one = np.zeros((H, W, 3), np.float32)
+        st1 = pt.doTrace(d, s.m_camera, None, spp, seed=7, radiance=one, band=band, pipe_sets=1,
+                         spp_per_launch=spp)
+        piped = np.zeros((H, W, 3), np.float32)
+        st2 = pt.doTrace(d, s.m_camera, None, spp, seed=7, radiance=piped, band=band, **kw)
+        assert st2["trace_launches"] > kw["pipe_sets"], st2   # several chunks per set
+        assert st1["traversals"] == st2["traversals"]
+        assert np.array_equal(_bits(piped), _bits(one))
+    finally:
+        d.close()
