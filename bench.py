@@ -89,11 +89,13 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong: one frame banded across the N ranks (gather); "
                          "weak: N frames per step, each banded across the N ranks (all-to-all)")
-    ap.add_argument("--deal", choices=["interleaved", "cost", "cost-heavy-first"], default="interleaved",
+    ap.add_argument("--deal", choices=["interleaved", "cost", "cost-heavy-first", "interleaved-sets", "cost-sets"],
+                    default="interleaved",
                     help="N > 1 (or --emulate-ranks): interleaved = band b -> rank b %% N (default); cost = bands "
                          "dealt by an untimed probe frame's measured band costs (shard.cost_deal; measured no better, "
                          "DESIGN.md section 6 'Band deals'); cost-heavy-first = the same, each rank's costliest "
-                         "bands dispatched first")
+                         "bands dispatched first; *-sets = that deal's bands ordered so the launch pipeline's three "
+                         "band sets carry equal probe costs (shard.set_balanced_order)")
     ap.add_argument("--weak-extra", type=int, default=1,
                     help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
     ap.add_argument("--fast-extra", type=int, default=1,
@@ -463,12 +465,19 @@ def main():
 
     deal, deal_info = None, None
     # (at N = 1, --deal cost-heavy-first orders the frame's own bands heaviest first)
-    if ((ranks > 1 and args.deal.startswith("cost")) or args.deal == "cost-heavy-first") and not args.wavefront:
+    if (((ranks > 1 and args.deal != "interleaved") or args.deal in ("cost-heavy-first", "interleaved-sets"))
+            and not args.wavefront):
         tp = time.perf_counter()
         costs = probe_costs()
         nbands = shard.n_bands(H, args.band_rows)
-        deal = shard.cost_deal(costs, ranks, order="heavy_first" if args.deal == "cost-heavy-first" else "ascending",
-                               short_band=nbands - 1 if H % args.band_rows else None)
+        short = nbands - 1 if H % args.band_rows else None
+        nset = args.pipe_sets if args.pipe_sets > 0 else 3   # (tpt_render's default band sets)
+        if args.deal == "interleaved-sets":
+            deal = [shard.set_balanced_order(b, costs, nset, short)
+                    for b in shard.interleaved_deal(H, args.band_rows, ranks)]
+        else:
+            order = {"cost-heavy-first": "heavy_first", "cost-sets": "sets"}.get(args.deal, "ascending")
+            deal = shard.cost_deal(costs, ranks, order=order, short_band=short, nset=nset)
         il = shard.deal_loads(costs, shard.interleaved_deal(H, args.band_rows, ranks))
         cl = shard.deal_loads(costs, deal)
         deal_info = {"kind": args.deal, "probe_s": round(time.perf_counter() - tp, 3),

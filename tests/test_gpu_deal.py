@@ -167,7 +167,8 @@ def test_full_size_c2_cost_deal_8_ways():
 
 @pytest.mark.parametrize("W,H,kw", [
     (256, 96, {"pipe_sets": 2, "pipe_chunks": 4}),                       # XCD runs of 2 tiles, 4 rotations per set
-    (640, 80, {"pipe_sets": 3, "pipe_chunks": 8, "band": (16, 2, 1)}),    # runs of 5, a strong-scaled share
+    (640, 160, {"pipe_sets": 3, "pipe_chunks": 8, "band": (16, 2, 1), "lanes_per_pixel": 1}),   # runs of 5, one lane,
+                                                                     # a strong-scaled share
 ])
 def test_xcd_runs_rotated_per_chunk_bit_identical(W, H, kw):
     """A scene larger than an XCD's L2 (c5, 131 K triangles) deals tiles to XCDs in
@@ -181,7 +182,7 @@ def test_xcd_runs_rotated_per_chunk_bit_identical(W, H, kw):
         band = kw.pop("band", (16, 1, 0))
         one = np.zeros((H, W, 3), np.float32)
         st1 = pt.doTrace(d, s.m_camera, None, spp, seed=7, radiance=one, band=band, pipe_sets=1,
-                         spp_per_launch=spp)
+                         spp_per_launch=spp, lanes_per_pixel=kw.get("lanes_per_pixel", 0))
         piped = np.zeros((H, W, 3), np.float32)
         st2 = pt.doTrace(d, s.m_camera, None, spp, seed=7, radiance=piped, band=band, **kw)
         assert st2["trace_launches"] > kw["pipe_sets"], st2   # several chunks per set

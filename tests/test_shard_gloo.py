@@ -121,6 +121,38 @@ def test_cost_deal_partitions_and_balances():
     assert shard.interleaved_deal(1080, 16, 8)[3] == list(range(3, 68, 8))
 
 
+def test_set_balanced_order():
+    """shard.set_balanced_order: a permutation of the rank's bands whose
+    list[k::nset] (tpt_render's band set k) are ascending, sized
+    ceil((n - k) / nset), with a short last band last; the sets' cost spread is
+    at most one band's cost, and no larger than the plain ascending order's."""
+    from tinypathtracer_amd import shard
+    rng = np.random.default_rng(11)
+    costs = rng.random(135) * 100.0
+    costs[[0, 134]] = 0.5   # nearly empty top and bottom bands, as at C5
+    for bands, nset, short in ((list(range(7, 135, 8)), 3, None), (list(range(0, 135, 8)), 3, None),
+                               (list(range(135)), 3, None), (list(range(3, 68, 4)), 2, 67), (list(range(9)), 4, 8),
+                               ([5], 3, None), ([], 3, None)):
+        o = shard.set_balanced_order(bands, costs, nset, short)
+        assert sorted(o) == sorted(bands)
+        if short is not None:
+            assert o[-1] == short
+        k_sets = min(nset, max(len(o), 1))
+        if len(o) <= 1:
+            continue
+        sets = [o[k::k_sets] for k in range(k_sets)]
+        assert all(s_ == sorted(s_, key=lambda b: (b == short, b)) for s_ in sets)
+        assert [len(s_) for s_ in sets] == [(len(o) - k + k_sets - 1) // k_sets for k in range(k_sets)]
+        loads = [sum(costs[b] for b in s_) for s_ in sets]
+        plain = sorted(bands, key=lambda b: (b == short, b))
+        ploads = [sum(costs[b] for b in plain[k::k_sets]) for k in range(k_sets)]
+        assert max(loads) - min(loads) <= max(costs[b] for b in bands) + 1e-9
+        assert max(loads) <= max(ploads) + 1e-9
+    # through cost_deal
+    d = shard.cost_deal(costs, 8, order="sets", nset=3)
+    assert sorted(b for r in d for b in r) == list(range(135))
+
+
 def _worker_deal(rank, world, port, out_path, deal):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"

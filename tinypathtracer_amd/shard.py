@@ -45,7 +45,7 @@ def max_band_height(height: int, band_rows: int, world: int, deal=None) -> int:
     return max(len(band_row_ids(height, band_rows, world, r, deal)) for r in range(world))
 
 
-def cost_deal(costs, world: int, max_iter: int = 2000, order: str = "ascending", short_band=None):
+def cost_deal(costs, world: int, max_iter: int = 2000, order: str = "ascending", short_band=None, nset: int = 3):
     """Bands -> ranks by their measured costs (one float per global band, e.g.
     the summed wave life tpt_params.band_cost reports for the previous frame):
     longest-processing-time first -- heaviest band to the least-loaded rank --
@@ -102,9 +102,50 @@ def cost_deal(costs, world: int, max_iter: int = 2000, order: str = "ascending",
             load[m] += c[j]
     if order == "ascending":
         return [sorted(o) for o in own]
+    if order == "sets":
+        return [set_balanced_order(o, c, nset, short_band) for o in own]
     if order != "heavy_first":
-        raise ValueError("order: ascending or heavy_first")
+        raise ValueError("order: ascending, heavy_first or sets")
     return [sorted(o, key=lambda b: (b == short_band, -c[b], b)) for o in own]
+
+
+def set_balanced_order(bands, costs, nset: int = 3, short_band=None):
+    """One rank's bands ordered so that the launch pipeline's band sets carry
+    equal costs.  tpt_render splits a listed share into nset sets on their own
+    streams, set k taking list entries k, k + nset, ... (api.cpp); the sets run
+    side by side and the last one to finish ends the frame, so a share whose
+    bands do not divide evenly -- or whose few light bands fall into one set --
+    ends on its heaviest set.  Set k gets ceil((n - k) / nset) slots; the bands
+    fill them longest-processing-time first (heaviest band to the least-loaded
+    set with a free slot); a short last band is placed in the set that holds
+    the list's last slot.  Each set keeps its bands in ascending order, and the
+    list interleaves the sets, so list[k::nset] is set k.  Deterministic."""
+    bands = [int(b) for b in bands]
+    n = len(bands)
+    if nset <= 1 or n <= 1:
+        return sorted(bands, key=lambda b: (b == short_band, b))
+    nset = min(nset, n)
+    size = [(n - k + nset - 1) // nset for k in range(nset)]
+    groups = [[] for _ in range(nset)]
+    load = [0.0] * nset
+    rest = bands
+    if short_band is not None and short_band in bands:
+        k = (n - 1) % nset
+        groups[k].append(short_band)
+        load[k] += float(costs[short_band])
+        rest = [b for b in bands if b != short_band]
+    for b in sorted(rest, key=lambda i: (-float(costs[i]), i)):
+        k = min((k for k in range(nset) if len(groups[k]) < size[k]), key=lambda k: (load[k], k))
+        groups[k].append(b)
+        load[k] += float(costs[b])
+    for g in groups:
+        g.sort(key=lambda b: (b == short_band, b))
+    out = []
+    for i in range(max(size)):
+        for k in range(nset):
+            if i < len(groups[k]):
+                out.append(groups[k][i])
+    return out
 
 
 def deal_loads(costs, deal):
