@@ -6,9 +6,10 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 LIB=$PWD/tinypathtracer_amd/variants/verify/libtpt.so
-for spec in "C3 4096" "C2 1024" "C4 8192" "C5 256"; do
+for spec in "C3 4096" "C3 4096 --env-is" "C2 1024" "C4 8192" "C5 256"; do
   set -- $spec
-  TPT_LIB=$LIB TPT_DEBUG_WAVES=gpurun_out/verify_$1.bin TPT_DEBUG_COUNTERS=1 timeout -k 10 400 python bench.py --config $1 --spp $2 \
-    --steps 1 --warmup 0 --cpu-baseline 0 > gpurun_out/verify_$1.json 2> gpurun_out/verify_$1.err || { echo "$1 FAILED"; tail -3 gpurun_out/verify_$1.err; exit 1; }
-  echo "$1 $(grep 'tpt counters' gpurun_out/verify_$1.err | tail -1 | awk '{print "mismatches", $27}')"
+  C=$1; SPP=$2; shift 2; T=$C; [ -n "$1" ] && T=${C}is
+  TPT_LIB=$LIB TPT_DEBUG_WAVES=gpurun_out/verify_$T.bin TPT_DEBUG_COUNTERS=1 timeout -k 10 400 python bench.py --config $C --spp $SPP \
+    --steps 1 --warmup 0 --cpu-baseline 0 --fast-extra 0 "$@" > gpurun_out/verify_$T.json 2> gpurun_out/verify_$T.err || { echo "$T FAILED"; tail -3 gpurun_out/verify_$T.err; exit 1; }
+  echo "$T $(grep 'tpt counters' gpurun_out/verify_$T.err | tail -1 | awk '{print "mismatches", $27}')"
 done
