@@ -22,6 +22,7 @@ steps, passes, lt, lw, lx, lp = c[8], c[12], c[25], c[26], c[27], c[28]
 tot = lt + lw + lx
 print(f"{sys.argv[3]} {sys.argv[1]}: steps {steps} passes {passes} steps/pass {steps / max(passes, 1):.2f} | lane-steps: traversing "
       f"{lt / tot:.3f} waiting-for-pass {lw / tot:.3f} no-work {lx / tot:.3f} | lanes per pass {lp / max(passes, 1):.1f} | "
-      f"shading ticks {c[6]} traversal ticks {c[7]}")
+      f"shading ticks {c[6]} traversal ticks {c[7]} | pass sections (consume, lights/probe set-up, after, unwind, "
+      f"camera, ray set-up): {' '.join(str(v) for v in c[17:23])}")
 PY
 done
