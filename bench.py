@@ -89,12 +89,13 @@ def parse():
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong: one frame banded across the N ranks (gather); "
                          "weak: N frames per step, each banded across the N ranks (all-to-all)")
-    ap.add_argument("--deal", choices=["interleaved", "cost", "cost-heavy-first", "interleaved-sets", "cost-sets"],
+    ap.add_argument("--deal", choices=["interleaved", "cost", "cost-heavy-first", "interleaved-sets", "cost-sets",
+                                       "interleaved-heavy-first"],
                     default="interleaved",
                     help="N > 1 (or --emulate-ranks): interleaved = band b -> rank b %% N (default); cost = bands "
                          "dealt by an untimed probe frame's measured band costs (shard.cost_deal; measured no better, "
                          "DESIGN.md section 6 'Band deals'); cost-heavy-first = the same, each rank's costliest "
-                         "bands dispatched first; *-sets = that deal's bands ordered so the launch pipeline's three "
+                         "bands dispatched first (interleaved-heavy-first: the interleave's); *-sets = that deal's bands ordered so the launch pipeline's three "
                          "band sets carry equal probe costs (shard.set_balanced_order)")
     ap.add_argument("--weak-extra", type=int, default=1,
                     help="N>1 with --scaling strong: also time weak scaling (key 'weak')")
@@ -465,7 +466,8 @@ def main():
 
     deal, deal_info = None, None
     # (at N = 1, --deal cost-heavy-first orders the frame's own bands heaviest first)
-    if (((ranks > 1 and args.deal != "interleaved") or args.deal in ("cost-heavy-first", "interleaved-sets"))
+    if (((ranks > 1 and args.deal != "interleaved") or args.deal in ("cost-heavy-first", "interleaved-sets",
+                                                                     "interleaved-heavy-first"))
             and not args.wavefront):
         tp = time.perf_counter()
         costs = probe_costs()
@@ -474,6 +476,9 @@ def main():
         nset = args.pipe_sets if args.pipe_sets > 0 else 3   # (tpt_render's default band sets)
         if args.deal == "interleaved-sets":
             deal = [shard.set_balanced_order(b, costs, nset, short)
+                    for b in shard.interleaved_deal(H, args.band_rows, ranks)]
+        elif args.deal == "interleaved-heavy-first":   # the interleave's bands, each rank's costliest first
+            deal = [sorted(b, key=lambda i: (i == short, -float(costs[i]), i))
                     for b in shard.interleaved_deal(H, args.band_rows, ranks)]
         else:
             order = {"cost-heavy-first": "heavy_first", "cost-sets": "sets"}.get(args.deal, "ascending")
