@@ -1363,13 +1363,7 @@ tpt_status tpt_render_frames(tpt_scene* s, const tpt_env* env, const tpt_camera*
     // Shallow trees (few triangles) make a traversal short against a shading
     // pass, so passes are batched harder there: tir (6 triangles) refill 16
     // 84.6 Grays/s vs 24 72.6-78.9; box (1,932) 16 = 24; C5 (131 K) 16 -3 %.
-    // Re-checked on round 6's final build (4 interleaved reps, gpurun_out/r06ad):
-    // box 20 15,868 against 16 15,753 and 24 15,806 Mrays/s; tir 16 87,923 against
-    // 20 79,281.  But box's strong-scaled N = 2 share (1 M pixels) takes 381-384 ms at
-    // 20 against 365-368 at 16 (gpurun_out/r06ae): the harder batching pays only in
-    // launches of at least four times the chip's resident lanes.
-    const int mid = launch_pix >= 4.0 * resident ? 20 : 16;
-    const int full = s->n_faces <= 64 ? 16 : (s->n_faces <= 4096 ? mid : 24);
+    const int full = s->n_faces <= 4096 ? 16 : 24;
     // Pair mode (round 3, after the 4-wave pair variants and the fp32-bounded env
     // lookup; C3 1080p 4096 spp, Mrays/s): refill 8 7,711, 6 7,720, 4 7,790-7,942,
     // 3 7,911-7,934, 2 7,860-7,983 -> 3; with env IS (the side lane's env sample
